@@ -1,0 +1,406 @@
+"""Python binding of libbzr.so (the MI355X-native Bezier-triangle ray tracer).
+
+Thin ctypes layer over the C ABI in include/bzr.h.  The hot path
+(BezierMesh::intersect, BezierTriangle::intersect, BezierLens::refract and the
+refraction chain; reference/bezierMesh.cpp:206-227, bezierTriangle.cpp:123-195,
+bezierLens.cpp:4-34, test.cpp:376-401) only exists as HIP kernels inside
+libbzr.so: there is no Python or CPU fallback, and importing this package
+raises if the library has not been built.
+
+Arrays: rays are float32 SoA [6, n] (ox, oy, oz, dx, dy, dz); hits are
+float32 [13, n] with rows t, px, py, pz, cos, b0, b1, b2, nx, ny, nz and the
+uint32 bit patterns of `what` and `patch` in rows 11 and 12.  Host numpy
+arrays or CUDA (HIP) torch tensors are accepted; tensors stay on the device
+and run asynchronously on the context's stream.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+import numpy as np
+
+PKG_DIR = Path(__file__).resolve().parent.parent
+LIB_PATH = PKG_DIR / "lib" / "libbzr.so"
+
+OK = 0
+HOST_PTRS, DEVICE_PTRS = 0, 1
+MODE_PARITY, MODE_FAST = 0, 2
+WHAT_FOLLOW0, WHAT_FOLLOW1, WHAT_FOLLOW2, WHAT_NONE, WHAT_INTERSECT = 0, 1, 2, 3, 4
+LIMIT_THIS, LIMIT_NONE = 0, 1
+RR_NONE, RR_INSIDE, RR_OUTSIDE = 0, 1, 2
+ENVELOPE_ELLIPSOID, ENVELOPE_TESTLENS = 0, 1
+PATCH_WORDS = 66  # sizeof(bzr_patch) / 4
+HIT_FIELDS = 13
+
+_P = ctypes.c_void_p
+_U32 = ctypes.c_uint32
+_I32 = ctypes.c_int32
+_F = ctypes.c_float
+
+# name -> argtypes (all return bzr_status = int32 unless listed in _RET)
+_SIGS = {
+    "bzr_abi_version": [],
+    "bzr_last_error": [],
+    "bzr_device_count": [ctypes.POINTER(_I32)],
+    "bzr_ctx_create": [_I32, ctypes.POINTER(_P)],
+    "bzr_ctx_destroy": [_P],
+    "bzr_ctx_set_stream": [_P, _P],
+    "bzr_ctx_use_own_stream": [_P],
+    "bzr_ctx_get_stream": [_P, ctypes.POINTER(_P)],
+    "bzr_sync": [_P],
+    "bzr_mesh_create": [_P, _P, _U32, _U32, ctypes.POINTER(_P)],
+    "bzr_mesh_destroy": [_P],
+    "bzr_mesh_size": [_P, ctypes.POINTER(_U32)],
+    "bzr_intersect": [_P, _P, _P, _U32, _P, _U32],
+    "bzr_patch_intersect": [_P, _P, _P, _P, _P, _U32, _P, _U32],
+    "bzr_refract": [_P, _P, _F, _P, _P, _U32, _U32, _P, _P, _U32],
+    "bzr_trace_chain": [_P, _P, _P, _U32, _P, _U32, _P, _P, _P, _U32],
+    "bzr_trimesh_create": [ctypes.POINTER(_P)],
+    "bzr_trimesh_destroy": [_P],
+    "bzr_trimesh_copy": [_P, ctypes.POINTER(_P)],
+    "bzr_trimesh_size": [_P, ctypes.POINTER(_U32)],
+    "bzr_trimesh_get": [_P, _P],
+    "bzr_trimesh_set": [_P, _P, _U32],
+    "bzr_trimesh_make_solid_of_revolution": [_P, _I32, _I32, _I32, _F, _F, _F],
+    "bzr_trimesh_make_ellipsoid": [_P, _I32, _I32, _F, _F, _F],
+    "bzr_trimesh_read_stl": [_P, ctypes.c_char_p],
+    "bzr_trimesh_write_stl": [_P, ctypes.c_char_p],
+    "bzr_trimesh_transform": [_P, _P, _P],
+    "bzr_trimesh_split": [_P, _I32],
+    "bzr_trimesh_split_maxside": [_P, _F],
+    "bzr_trimesh_standardize_vertices": [_P],
+    "bzr_trimesh_standardize_normals": [_P],
+    "bzr_trimesh_neighbours": [_P, _P, _P],
+    "bzr_bezier_build": [_P, _P],
+    "bzr_bezier_split_thick": [_P, _P],
+    "bzr_bezier_interpolate": [_P, _I32, _P],
+}
+_RET = {"bzr_last_error": ctypes.c_char_p, "bzr_abi_version": _I32}
+
+_lib = None
+
+
+class BzrError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libbzr.so (raises BzrError if it has not been built).
+
+    PyTorch-ROCm ships its own libamdhip64 / libhsa-runtime64.  If libbzr were loaded first it
+    would bind /opt/rocm's copies and torch would then load a second HIP runtime into the process
+    (torch reports "No HIP GPUs are available").  Importing torch first (when installed) makes
+    libbzr bind the runtime torch already loaded: one HIP runtime per process."""
+    global _lib
+    if _lib is None:
+        if os.environ.get("BZR_NO_TORCH_PRELOAD") != "1":
+            try:
+                import torch  # noqa: F401
+            except ImportError:
+                pass
+        if not LIB_PATH.exists():
+            raise BzrError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+        handle = ctypes.CDLL(str(LIB_PATH))
+        for name, args in _SIGS.items():
+            fn = getattr(handle, name)
+            fn.argtypes = args
+            fn.restype = _RET.get(name, _I32)
+        _lib = handle
+    return _lib
+
+
+def exported_symbols():
+    return list(_SIGS)
+
+
+def _check(status: int):
+    if status != OK:
+        msg = lib().bzr_last_error().decode(errors="replace")
+        raise BzrError(f"libbzr status {status}: {msg}")
+
+
+def device_count() -> int:
+    c = _I32(0)
+    _check(lib().bzr_device_count(ctypes.byref(c)))
+    return c.value
+
+
+# --------------------------------------------------------------- buffers
+def _is_tensor(x) -> bool:
+    return hasattr(x, "data_ptr") and hasattr(x, "is_cuda")
+
+
+class _Buf:
+    """Pointer + residency of a numpy array or a torch tensor."""
+
+    def __init__(self, x, dtype, writable=False):
+        if x is None:
+            self.ptr, self.device, self.keep = None, None, None
+            return
+        if _is_tensor(x):
+            if not x.is_contiguous():
+                raise BzrError("tensor arguments must be contiguous")
+            want = {np.float32: "torch.float32", np.uint32: "torch.uint32", np.int32: "torch.int32"}
+            if str(x.dtype) not in (want[dtype], "torch.int32" if dtype == np.uint32 else want[dtype]):
+                raise BzrError(f"tensor dtype {x.dtype} where {want[dtype]} is expected")
+            self.ptr, self.device, self.keep = x.data_ptr(), bool(x.is_cuda), x
+        else:
+            a = np.asarray(x)
+            if a.dtype != dtype or not a.flags["C_CONTIGUOUS"]:
+                if writable:
+                    raise BzrError(f"output array must be C-contiguous {np.dtype(dtype).name}")
+                a = np.ascontiguousarray(a, dtype=dtype)
+            self.ptr, self.device, self.keep = a.ctypes.data, False, a
+
+
+def _residency(*bufs) -> int:
+    flags = {b.device for b in bufs if b.device is not None}
+    if len(flags) != 1:
+        raise BzrError("mix of host and device buffers in one call")
+    return DEVICE_PTRS if flags.pop() else HOST_PTRS
+
+
+# --------------------------------------------------------------- context
+class Context:
+    """A HIP device + stream (bzr_ctx)."""
+
+    def __init__(self, device: int = 0):
+        h = _P()
+        _check(lib().bzr_ctx_create(device, ctypes.byref(h)))
+        self.handle = h
+        self.device = device
+
+    def set_stream(self, stream_ptr: int | None):
+        """Launch on this hipStream_t (0 / None = the HIP null stream); None-safe."""
+        _check(lib().bzr_ctx_set_stream(self.handle, stream_ptr or None))
+
+    def use_own_stream(self):
+        _check(lib().bzr_ctx_use_own_stream(self.handle))
+
+    def use_torch_stream(self, stream=None):
+        """Launch on a torch stream (default: torch's current stream, which may be the null stream),
+        so torch ops and torch.cuda.Event timing order with the kernels."""
+        import torch
+
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        self.set_stream(s.cuda_stream)
+
+    def sync(self):
+        _check(lib().bzr_sync(self.handle))
+
+    def close(self):
+        if getattr(self, "handle", None):
+            lib().bzr_ctx_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class DeviceMesh:
+    """Immutable device copy of a patch array (bzr_mesh): float32 [n, 66] records."""
+
+    def __init__(self, ctx: Context, patches: np.ndarray):
+        p = np.ascontiguousarray(patches, dtype=np.float32).reshape(-1, PATCH_WORDS)
+        h = _P()
+        _check(lib().bzr_mesh_create(ctx.handle, p.ctypes.data if len(p) else None, len(p), PATCH_WORDS * 4,
+                                     ctypes.byref(h)))
+        self.handle, self.ctx, self.n = h, ctx, len(p)
+
+    def close(self):
+        if getattr(self, "handle", None):
+            lib().bzr_mesh_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _n_of(rays) -> int:
+    shape = tuple(rays.shape)
+    if len(shape) != 2 or shape[0] != 6:
+        raise BzrError(f"rays must be [6, n], got {shape}")
+    return int(shape[1])
+
+
+def _empty_like(rays, rows, dtype):
+    n = _n_of(rays)
+    if _is_tensor(rays):
+        import torch
+
+        tdt = {np.float32: torch.float32, np.uint32: torch.int32}[dtype]
+        return torch.empty((rows, n) if rows else (n,), dtype=tdt, device=rays.device)
+    return np.empty((rows, n) if rows else (n,), dtype=dtype)
+
+
+def intersect(ctx: Context, mesh: DeviceMesh, rays, out=None, mode=MODE_PARITY):
+    """BezierMesh::intersect over a batch -> hits [13, n]."""
+    n = _n_of(rays)
+    out = _empty_like(rays, HIT_FIELDS, np.float32) if out is None else out
+    r, o = _Buf(rays, np.float32), _Buf(out, np.float32, True)
+    _check(lib().bzr_intersect(ctx.handle, mesh.handle, r.ptr, n, o.ptr, _residency(r, o) | mode))
+    return out
+
+
+def patch_intersect(ctx: Context, mesh: DeviceMesh, patch_index, limit, rays, out=None):
+    """BezierTriangle::intersect for (patch, ray, limit) triples -> hits [13, n]."""
+    n = _n_of(rays)
+    out = _empty_like(rays, HIT_FIELDS, np.float32) if out is None else out
+    i, l_ = _Buf(patch_index, np.uint32), _Buf(limit, np.uint32)
+    r, o = _Buf(rays, np.float32), _Buf(out, np.float32, True)
+    _check(lib().bzr_patch_intersect(ctx.handle, mesh.handle, i.ptr, l_.ptr, r.ptr, n, o.ptr, _residency(i, l_, r, o)))
+    return out
+
+
+def refract(ctx: Context, mesh: DeviceMesh, ri: float, rays, expected=None, expected_all=RR_INSIDE,
+            out_rays=None, out_status=None):
+    """BezierLens::refract over a batch -> (rays [6, n], status [n])."""
+    n = _n_of(rays)
+    out_rays = _empty_like(rays, 6, np.float32) if out_rays is None else out_rays
+    out_status = _empty_like(rays, 0, np.uint32) if out_status is None else out_status
+    r, e = _Buf(rays, np.float32), _Buf(expected, np.uint32)
+    o, s = _Buf(out_rays, np.float32, True), _Buf(out_status, np.uint32, True)
+    _check(lib().bzr_refract(ctx.handle, mesh.handle, float(ri), r.ptr, e.ptr, int(expected_all), n, o.ptr, s.ptr,
+                             _residency(r, o, s, *([e] if expected is not None else []))))
+    return out_rays, out_status
+
+
+def trace_chain(ctx: Context, lenses, ri, rays, out_rays=None, out_status=None, out_segments=None):
+    """Refraction chain through `lenses` (list of DeviceMesh) -> (rays [6, n], status [n], segments [n])."""
+    n = _n_of(rays)
+    nl = len(lenses)
+    handles = (_P * nl)(*[m.handle for m in lenses])
+    ris = (_F * nl)(*[float(x) for x in ri])
+    out_rays = _empty_like(rays, 6, np.float32) if out_rays is None else out_rays
+    out_status = _empty_like(rays, 0, np.uint32) if out_status is None else out_status
+    out_segments = _empty_like(rays, 0, np.uint32) if out_segments is None else out_segments
+    r = _Buf(rays, np.float32)
+    o, s, g = _Buf(out_rays, np.float32, True), _Buf(out_status, np.uint32, True), _Buf(out_segments, np.uint32, True)
+    _check(lib().bzr_trace_chain(ctx.handle, handles, ris, nl, r.ptr, n, o.ptr, s.ptr, g.ptr, _residency(r, o, s, g)))
+    return out_rays, out_status, out_segments
+
+
+# ------------------------------------------------------------ host preprocessing
+class TriMesh:
+    """The reference's Mesh (host C++ in libbzr): generators, welding, orientation, Bezier build."""
+
+    def __init__(self, _handle=None):
+        if _handle is None:
+            h = _P()
+            _check(lib().bzr_trimesh_create(ctypes.byref(h)))
+            _handle = h
+        self.handle = _handle
+
+    def __del__(self):
+        try:
+            if getattr(self, "handle", None):
+                lib().bzr_trimesh_destroy(self.handle)
+                self.handle = None
+        except Exception:
+            pass
+
+    def copy(self) -> "TriMesh":
+        h = _P()
+        _check(lib().bzr_trimesh_copy(self.handle, ctypes.byref(h)))
+        return TriMesh(h)
+
+    def __len__(self):
+        n = _U32(0)
+        _check(lib().bzr_trimesh_size(self.handle, ctypes.byref(n)))
+        return n.value
+
+    @property
+    def triangles(self) -> np.ndarray:
+        t = np.empty((len(self), 3, 3), dtype=np.float32)
+        _check(lib().bzr_trimesh_get(self.handle, t.ctypes.data))
+        return t
+
+    @triangles.setter
+    def triangles(self, tris):
+        t = np.ascontiguousarray(tris, dtype=np.float32).reshape(-1, 3, 3)
+        _check(lib().bzr_trimesh_set(self.handle, t.ctypes.data, len(t)))
+
+    def make_ellipsoid(self, sectors, belts, size=(1.0, 1.0, 1.0)):
+        _check(lib().bzr_trimesh_make_ellipsoid(self.handle, sectors, belts, *map(float, size)))
+        return self
+
+    def make_unit_sphere(self, sectors, belts):
+        return self.make_ellipsoid(sectors, belts, (1.0, 1.0, 1.0))
+
+    def make_solid_of_revolution(self, sectors, belts, envelope, size):
+        _check(lib().bzr_trimesh_make_solid_of_revolution(self.handle, sectors, belts, envelope, *map(float, size)))
+        return self
+
+    def read_stl(self, path):
+        _check(lib().bzr_trimesh_read_stl(self.handle, str(path).encode()))
+        return self
+
+    def write_stl(self, path):
+        _check(lib().bzr_trimesh_write_stl(self.handle, str(path).encode()))
+        return self
+
+    def transform(self, matrix=None, displacement=(0.0, 0.0, 0.0)):
+        m = np.eye(3, dtype=np.float32) if matrix is None else np.asarray(matrix, dtype=np.float32)
+        colmajor = np.ascontiguousarray(m.T.reshape(-1))
+        d = np.ascontiguousarray(displacement, dtype=np.float32)
+        _check(lib().bzr_trimesh_transform(self.handle, colmajor.ctypes.data, d.ctypes.data))
+        return self
+
+    def translate(self, d):
+        return self.transform(None, d)
+
+    def split(self, divisor: int):
+        _check(lib().bzr_trimesh_split(self.handle, divisor))
+        return self
+
+    def split_maxside(self, max_side: float):
+        _check(lib().bzr_trimesh_split_maxside(self.handle, float(max_side)))
+        return self
+
+    def standardize_vertices(self):
+        _check(lib().bzr_trimesh_standardize_vertices(self.handle))
+        return self
+
+    def standardize_normals(self):
+        _check(lib().bzr_trimesh_standardize_normals(self.handle))
+        return self
+
+    def standardize(self):
+        return self.standardize_vertices().standardize_normals()
+
+    def neighbours(self):
+        n = len(self)
+        fellow = np.empty((n, 3), dtype=np.uint32)
+        start = np.empty((n, 3), dtype=np.uint8)
+        _check(lib().bzr_trimesh_neighbours(self.handle, fellow.ctypes.data, start.ctypes.data))
+        return fellow, start
+
+    def bezier_patches(self) -> np.ndarray:
+        """BezierMesh(Mesh) -> float32 [3n, 66] patch records (bzr_patch layout)."""
+        out = np.empty((3 * len(self), PATCH_WORDS), dtype=np.float32)
+        _check(lib().bzr_bezier_build(self.handle, out.ctypes.data))
+        return out
+
+    def bezier_split_thick(self) -> "TriMesh":
+        out = TriMesh()
+        _check(lib().bzr_bezier_split_thick(self.handle, out.handle))
+        return out
+
+    def bezier_interpolate(self, divisor: int) -> "TriMesh":
+        out = TriMesh()
+        _check(lib().bzr_bezier_interpolate(self.handle, divisor, out.handle))
+        return out
+
+
+__all__ = [
+    "BzrError", "Context", "DeviceMesh", "TriMesh", "intersect", "patch_intersect", "refract", "trace_chain",
+    "device_count", "lib", "exported_symbols", "LIB_PATH",
+]

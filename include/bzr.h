@@ -1,0 +1,160 @@
+/*
+ * bzr.h -- C ABI of the MI355X-native Bezier-triangle ray tracer (libbzr.so).
+ *
+ * The reference (balazs-bamer/cuda-bezier-triangle-raytracer @ v1) has no FFI;
+ * its boundary is the C++ class API it exports for this path:
+ *   BezierMesh::intersect(Ray)          reference/bezierMesh.h:37, bezierMesh.cpp:206-227
+ *   BezierTriangle::intersect(Ray, lim) reference/bezierTriangle.h:105, bezierTriangle.cpp:123-195
+ *   BezierLens::refract(Ray, expected)  reference/bezierLens.h:27, bezierLens.cpp:4-34
+ *   the refraction-chain driver loop    reference/test.cpp:376-401
+ * plus the host preprocessing that produces the patch records
+ *   Mesh                                reference/mesh.h:18-133
+ *   BezierMesh::BezierMesh(Mesh)        reference/bezierMesh.cpp:4-51
+ * Every entry point below is the batch form of one of those, with plain
+ * pointers and sizes.  The C++ drop-in classes in include/bzr/bzr.hpp forward
+ * to it; INTEGRATION.md shows the binding a maintainer adds.
+ *
+ * Conventions
+ *   - Every call returns bzr_status (0 = ok).  Nothing throws across the ABI.
+ *     bzr_last_error() returns the calling thread's last error text.
+ *   - Rays are SoA: rays_soa[k*n + i], k = 0..5 -> ox, oy, oz, dx, dy, dz.
+ *     Directions are used as given (the reference's Ray ctor normalises;
+ *     normalise on the caller side exactly as Ray(start, dir) does).
+ *   - Hits are SoA, 13 words per ray: hits_soa[k*n + i] with k =
+ *       0 t   1 px  2 py  3 pz  4 cos  5 b0  6 b1  7 b2  8 nx  9 ny  10 nz
+ *       11 what (uint32: 0..2 follow side, 3 none, 4 intersect)
+ *       12 patch (uint32: index of the patch hit, 0xFFFFFFFF on a miss)
+ *     On a miss t = FLT_MAX and fields 1..10 are 0 (the reference leaves them
+ *     uninitialised).
+ *   - Pointer residency is selected per call by BZR_DEVICE_PTRS; host-pointer
+ *     calls are synchronous, device-pointer calls are asynchronous on the
+ *     context's stream until bzr_sync().
+ *   - Numerics: BZR_MODE_PARITY (default) evaluates in IEEE binary32 with the
+ *     reference's operation order and no contraction, bit-identical to the
+ *     CPU oracle.  BZR_MODE_FAST allows FMA contraction in the Newton stage.
+ */
+#ifndef BZR_H
+#define BZR_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BZR_ABI_VERSION 1
+
+typedef int32_t bzr_status;
+enum {
+  BZR_OK = 0,
+  BZR_ERR_INVALID_ARGUMENT = 1,
+  BZR_ERR_HIP = 2,
+  BZR_ERR_OUT_OF_MEMORY = 3,
+  BZR_ERR_PREPROCESS = 4,   /* a reference preprocessing "throw" (e.g. "Vertex on edge detected.") */
+  BZR_ERR_NO_DEVICE = 5
+};
+
+enum {
+  BZR_HOST_PTRS = 0u,
+  BZR_DEVICE_PTRS = 1u,
+  BZR_MODE_PARITY = 0u,
+  BZR_MODE_FAST = 2u
+};
+
+enum { BZR_WHAT_FOLLOW0 = 0, BZR_WHAT_FOLLOW1 = 1, BZR_WHAT_FOLLOW2 = 2, BZR_WHAT_NONE = 3, BZR_WHAT_INTERSECT = 4 };
+enum { BZR_LIMIT_THIS = 0, BZR_LIMIT_NONE = 1 };                       /* BezierTriangle::LimitPlaneIntersection */
+enum { BZR_RR_NONE = 0, BZR_RR_INSIDE = 1, BZR_RR_OUTSIDE = 2 };       /* RefractionResult */
+enum { BZR_HIT_FIELDS = 13, BZR_RAY_FIELDS = 6 };
+
+/* One cubic Bezier patch, byte-identical to the reference's BezierTriangle
+ * (reference/bezierTriangle.h:64-80; Eigen column-major 3x3): 264 bytes. */
+typedef struct bzr_patch {
+  float    under_n[3], under_c;        /* mUnderlyingPlane                  @0   */
+  float    divider[3][4];              /* mNeighbourDividerPlanes (n, c)    @16  */
+  uint32_t neigh[3];                   /* mNeighbours                       @64  */
+  float    cp[10][3];                  /* mControlPoints                    @76  */
+  float    minv[9];                    /* mBarycentricInverse, col-major    @196 */
+  float    h_in, h_out;                /* mHeightInside / mHeightOutside    @232 */
+  float    dir_a[3], dir_b[3];         /* derivative direction vectors      @240 */
+} bzr_patch;
+
+typedef struct bzr_ctx bzr_ctx;         /* one HIP device + one stream; one host thread at a time */
+typedef struct bzr_mesh bzr_mesh;       /* immutable device copy of a patch array */
+typedef struct bzr_trimesh bzr_trimesh; /* host triangle mesh (reference Mesh) */
+
+/* ---- library ---- */
+int32_t     bzr_abi_version(void);
+const char *bzr_last_error(void);
+bzr_status  bzr_device_count(int32_t *count);
+
+/* ---- context ---- */
+bzr_status bzr_ctx_create(int32_t hip_device, bzr_ctx **out);
+bzr_status bzr_ctx_destroy(bzr_ctx *ctx);
+/* Launch on a caller-owned hipStream_t (NULL = the HIP null stream);
+ * bzr_ctx_use_own_stream() goes back to the context's own non-blocking stream. */
+bzr_status bzr_ctx_set_stream(bzr_ctx *ctx, void *hip_stream);
+bzr_status bzr_ctx_use_own_stream(bzr_ctx *ctx);
+bzr_status bzr_ctx_get_stream(bzr_ctx *ctx, void **hip_stream);
+bzr_status bzr_sync(bzr_ctx *ctx);
+
+/* ---- device mesh: BezierMesh's patch vector (reference/bezierMesh.h:17) ---- */
+/* Copies n records of `stride` bytes (stride >= sizeof(bzr_patch)) from host memory. */
+bzr_status bzr_mesh_create(bzr_ctx *ctx, const void *patches, uint32_t n, uint32_t stride, bzr_mesh **out);
+bzr_status bzr_mesh_destroy(bzr_mesh *mesh);
+bzr_status bzr_mesh_size(const bzr_mesh *mesh, uint32_t *n);
+
+/* ---- hot path ---- */
+/* BezierMesh::intersect over a ray batch (reference/bezierMesh.cpp:206-227). */
+bzr_status bzr_intersect(bzr_ctx *ctx, const bzr_mesh *mesh, const float *rays_soa, uint32_t n,
+                         float *hits_soa, uint32_t flags);
+/* BezierTriangle::intersect for (patch, ray, limit) triples (reference/bezierTriangle.cpp:123-195).
+ * The `patch` field of the output is the input patch index. */
+bzr_status bzr_patch_intersect(bzr_ctx *ctx, const bzr_mesh *mesh, const uint32_t *patch_index,
+                               const uint32_t *limit, const float *rays_soa, uint32_t n,
+                               float *hits_soa, uint32_t flags);
+/* BezierLens::refract (reference/bezierLens.cpp:4-34); expected may be NULL (then every ray expects
+ * `expected_all`).  out_rays_soa: the refracted ray (start = hit point) when status != NONE,
+ * the input ray otherwise. */
+bzr_status bzr_refract(bzr_ctx *ctx, const bzr_mesh *mesh, float refractive_index, const float *rays_soa,
+                       const uint32_t *expected, uint32_t expected_all, uint32_t n,
+                       float *out_rays_soa, uint32_t *out_status, uint32_t flags);
+/* The reference refraction chain (reference/test.cpp:376-401): for each lens, refract(INSIDE) then
+ * refract(OUTSIDE); a NONE terminates the ray.  out_rays_soa: ray after the last successful
+ * refraction (input ray if none); out_status: last status (OUTSIDE = passed every lens);
+ * out_segments (may be NULL): BezierMesh::intersect calls made for the ray. */
+bzr_status bzr_trace_chain(bzr_ctx *ctx, const bzr_mesh *const *lenses, const float *refractive_index,
+                           uint32_t nlens, const float *rays_soa, uint32_t n, float *out_rays_soa,
+                           uint32_t *out_status, uint32_t *out_segments, uint32_t flags);
+
+/* ---- host preprocessing (reference Mesh / BezierMesh construction) ---- */
+enum { BZR_ENVELOPE_ELLIPSOID = 0, BZR_ENVELOPE_TESTLENS = 1 };
+bzr_status bzr_trimesh_create(bzr_trimesh **out);
+bzr_status bzr_trimesh_destroy(bzr_trimesh *m);
+bzr_status bzr_trimesh_copy(const bzr_trimesh *src, bzr_trimesh **out);
+bzr_status bzr_trimesh_size(const bzr_trimesh *m, uint32_t *n);
+bzr_status bzr_trimesh_get(const bzr_trimesh *m, float *xyz /* 9*n */);
+bzr_status bzr_trimesh_set(bzr_trimesh *m, const float *xyz, uint32_t n);
+bzr_status bzr_trimesh_make_solid_of_revolution(bzr_trimesh *m, int32_t sectors, int32_t belts, int32_t envelope,
+                                                float sx, float sy, float sz);
+bzr_status bzr_trimesh_make_ellipsoid(bzr_trimesh *m, int32_t sectors, int32_t belts, float sx, float sy, float sz);
+bzr_status bzr_trimesh_read_stl(bzr_trimesh *m, const char *path);
+bzr_status bzr_trimesh_write_stl(const bzr_trimesh *m, const char *path);
+bzr_status bzr_trimesh_transform(bzr_trimesh *m, const float transform_colmajor[9], const float displacement[3]);
+bzr_status bzr_trimesh_split(bzr_trimesh *m, int32_t divisor);
+bzr_status bzr_trimesh_split_maxside(bzr_trimesh *m, float max_side);
+bzr_status bzr_trimesh_standardize_vertices(bzr_trimesh *m);
+bzr_status bzr_trimesh_standardize_normals(bzr_trimesh *m);
+/* Face neighbours after standardize_normals: 3 fellow indices + 3 common-side starts per face. */
+bzr_status bzr_trimesh_neighbours(const bzr_trimesh *m, uint32_t *fellow /* 3*n */, uint8_t *start /* 3*n */);
+/* BezierMesh(Mesh): writes 3*n patches. */
+bzr_status bzr_bezier_build(const bzr_trimesh *m, bzr_patch *out);
+/* BezierMesh::splitThickBezierTriangles -> new (unstandardized) triangle mesh */
+bzr_status bzr_bezier_split_thick(const bzr_trimesh *m, bzr_trimesh *out);
+/* BezierMesh::interpolate(divisor) -> tessellated triangle mesh */
+bzr_status bzr_bezier_interpolate(const bzr_trimesh *m, int32_t divisor, bzr_trimesh *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1153,22 +1153,48 @@ ohit orc_patch_intersect(const opatch *p, const oray *r, int limit) {
   return res;
 }
 
+/* Work counters (planar tests, Newton runs incl. follow-side retries) for the roofline's
+ * algorithmic flop count; updated once per BezierMesh::intersect call. */
+static uint64_t g_cnt_tests, g_cnt_newton, g_cnt_follow, g_cnt_segments;
+void orc_counters(uint64_t out[4]) { out[0] = g_cnt_tests; out[1] = g_cnt_newton; out[2] = g_cnt_follow; out[3] = g_cnt_segments; }
+void orc_counters_reset(void) { g_cnt_tests = g_cnt_newton = g_cnt_follow = g_cnt_segments = 0; }
+
+static int planar_candidate(const opatch *p, const oray *r) {
+  ov3 ip; float ic, it;
+  int valid = orc_plane_intersect_ray(p->under, r->start, r->dir, &ip, &ic, &it);
+  if (!(valid && fabsf(it) > -p->h_in && fabsf(it) > p->h_out)) return 0;
+  ov3 b = orc_matvec(p->minv, ip);
+  return b.x >= 0.0f && b.x <= 1.0f && b.y >= 0.0f && b.y <= 1.0f && b.z >= 0.0f && b.z <= 1.0f;
+}
+
 /* BezierMesh::intersect, reference/bezierMesh.cpp:206-227 */
 ohit orc_mesh_intersect(const opatch *p, uint32_t np, const oray *r) {
+  uint64_t newton = 0, follow = 0;
   ohit best;
   memset(&best, 0, sizeof best);
   best.t = FLT_MAX;
   best.what = ORC_NONE;
   best.patch = ~0u;
   for (uint32_t i = 0; i < np; ++i) {
+    if (!planar_candidate(&p[i], r)) continue;   /* same gate as the first lines of orc_patch_intersect */
+    ++newton;
     ohit c = orc_patch_intersect(&p[i], r, ORC_LIMIT_THIS);
     uint32_t src = i;
     if (c.what <= ORC_FOLLOW2) {
       src = p[i].neigh[c.what];
+      ++follow;
       c = orc_patch_intersect(&p[src], r, ORC_LIMIT_NONE);
     }
     if (c.what == ORC_INTERSECT && c.t < best.t) { best = c; best.patch = src; }
   }
+#pragma omp atomic
+  g_cnt_tests += np;
+#pragma omp atomic
+  g_cnt_newton += newton;
+#pragma omp atomic
+  g_cnt_follow += follow;
+#pragma omp atomic
+  g_cnt_segments += 1;
   return best;
 }
 

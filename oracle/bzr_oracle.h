@@ -143,6 +143,10 @@ void     orc_trace_chain_batch(const opatch *const *lens_patches, const uint32_t
 void     orc_refract_batch(const opatch *p, uint32_t np, float ri, const float *rays_soa, const uint32_t *expected,
                            uint32_t n, float *out_rays_soa, uint32_t *out_status, int threads);
 
+/* work counters since the last reset: planar tests, Newton runs, follow-side retries, intersect calls */
+void     orc_counters(uint64_t out[4]);
+void     orc_counters_reset(void);
+
 /* ---- reference/test.cpp:429-460 measureApproximation (the 7 published KATs) ---- */
 int      orc_measure_approximation(uint32_t split_steps, int32_t sectors, int32_t belts, ov3 size,
                                    int32_t divisor, float *out_error);
