@@ -4,14 +4,16 @@
 Workload (BASELINE.json configs[1]): makeEllipsoid(32,16,(1,4,2)) lens at x=10,
 refractive index 1.3, 1024x1024 primary rays along +x from the plane x=0 over y in [-4.2,4.2],
 z in [-2.1,2.1]; each ray runs refract(INSIDE) then refract(OUTSIDE) (reference/test.cpp:376-401).
-"Rays" counts every BezierMesh::intersect call (primary + refracted segments).
+"Rays" counts every BezierMesh::intersect call (primary + refracted segments).  --config cfg4 runs
+the two-lens 4096x4096 chain instead.
 
-A step = one frame: the whole chain over this rank's primary rays, inputs already resident in HBM.
-N GPUs = N processes (torch.distributed over RCCL): weak scaling -- the global image grows to
-side x (side*N) pixels, 64x64 tiles dealt round-robin to ranks, each rank tracing side^2 rays; the
-frame's results are gathered to rank 0 over RCCL inside the timed step (--gather step, default).
+A step = one frame: the whole chain over this rank's primary rays, inputs already resident in HBM,
+results bit-identical to the reference restatement (tests/test_gpu_parity.py).  N GPUs = N processes
+(torch.distributed over RCCL): weak scaling -- the image grows to side x (side*N) pixels, 64x64
+tiles dealt round-robin, side^2 rays per rank, and each frame's results are gathered to rank 0 over
+RCCL inside the timed step (--gather step, the default).
 
-Prints ONE JSON line on rank 0 (see the repository contract in DESIGN.md, section Measurement).
+Prints ONE JSON line on rank 0; fields are described in DESIGN.md (Measurement).
 """
 from __future__ import annotations
 
@@ -30,8 +32,10 @@ sys.path.insert(0, str(REPO))
 
 VALU_PEAK_TFLOPS = 157.3      # MI355X FP32 vector peak (MI355X_MICROARCH.md, chip parameters)
 HBM_PEAK_GBS = 8000.0         # MI355X HBM3E peak (spec)
-FLOPS_PLANAR = 33.0           # algorithmic flops per (segment, patch) planar test (SURVEY 8d)
-FLOPS_NEWTON = 1750.0         # algorithmic flops per Newton candidate (bracket + 4 iterations + tail)
+FLOPS_PLANAR = 33.0           # algorithmic flops per (segment, patch) planar test (SURVEY.md 8d)
+FLOPS_NEWTON = 1750.0         # algorithmic flops per Newton candidate: bracket + 4 iterations + tail
+FLOPS_REFRACT = 30.0          # Snell step per segment
+BYTES_PER_PRIMARY = 24 + 32   # ray in; ray + status + segment count out
 
 
 def parse():
@@ -42,19 +46,21 @@ def parse():
     p.add_argument("--config", default="cfg2", choices=["cfg2", "cfg4"])
     p.add_argument("--side", type=int, default=0, help="override rays per image side (per rank)")
     p.add_argument("--gather", default="step", choices=["step", "none"])
+    p.add_argument("--accel", default="bvh", choices=["bvh", "none"], help="none = brute-force scan (A/B)")
     p.add_argument("--cpu-baseline", default="on", choices=["on", "off"])
     p.add_argument("--cpu-sample-stride", type=int, default=2, help="oracle sample: every k-th row and column")
     return p.parse_args()
 
 
-def cpu_baseline(cfg, patches, ris, stride):
-    """The oracle (CPU restatement, test infrastructure) on a strided sample of the same workload."""
+def cpu_baseline(cfg, side, patches, ris, stride):
+    """The oracle (CPU restatement, test infrastructure) on a strided sample of the same workload;
+    also returns its work counters (planar tests, Newton runs) used for the algorithmic flop count."""
     from bzr_amd.configs import pixel_coords, rays_for
     from oracle import pyoracle
 
-    r, c = pixel_coords(cfg, order="rows")
+    r, c = pixel_coords(cfg, side=side, order="rows")
     keep = (r % stride == 0) & (c % stride == 0)
-    rays = rays_for(cfg, r[keep], c[keep])
+    rays = rays_for(cfg, r[keep], c[keep], side=side)
     threads = min(16, os.cpu_count() or 1)
     pyoracle.counters_reset()
     t0 = time.perf_counter()
@@ -66,8 +72,8 @@ def cpu_baseline(cfg, patches, ris, stride):
         "unit": "Mrays/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{rays.shape[1]} primaries (every {stride}th row and column of the {cfg.side}^2 grid), "
-                  f"{int(seg.sum())} segments, {dt:.2f} s wall, oracle/bzr_oracle.c -O2 OpenMP",
+        "sample": f"{rays.shape[1]} primaries (every {stride}th row and column of the {side}^2 grid), "
+                  f"{int(seg.sum())} segments, {dt:.2f} s wall; oracle/bzr_oracle.c -O2, OpenMP {threads} threads",
     }, cnt
 
 
@@ -77,54 +83,52 @@ def main():
     import torch.distributed as dist
 
     import bzr_amd
-    from bzr_amd.configs import CONFIGS, build_lens, rays_for, shard_pixels
+    from bzr_amd import frame
+    from bzr_amd.configs import CONFIGS, build_lens
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
 
     cfg = CONFIGS[a.config]
     side = a.side or cfg.side
     t0 = time.perf_counter()
     patches = [build_lens(bzr_amd.TriMesh, lens).bezier_patches() for lens in cfg.lenses]
-    prep_s = time.perf_counter() - t0
     ris = [lens.ri for lens in cfg.lenses]
+    prep_s = time.perf_counter() - t0
     n_patch = sum(len(p) for p in patches)
 
     ctx = bzr_amd.Context(local)
-    meshes = [bzr_amd.DeviceMesh(ctx, p) for p in patches]
+    t0 = time.perf_counter()
+    meshes = [bzr_amd.DeviceMesh(ctx, p) for p in patches]  # upload + BVH build
+    upload_s = time.perf_counter() - t0
     stream = torch.cuda.Stream(dev)   # one stream for the kernels, torch ops and the timing events
     torch.cuda.set_stream(stream)
     ctx.use_torch_stream(stream)
+    mode = bzr_amd.ACCEL_NONE if a.accel == "none" else bzr_amd.MODE_PARITY
 
-    # this rank's tiles of a side-wide, (side*world)-tall image (weak scaling: side^2 rays per rank)
-    from dataclasses import replace
-    rows, cols = shard_pixels(cfg, rank, world, side=side, height=side * world)
-    rays_np = rays_for(cfg, rows, cols, side=side, height=side * world)
+    _, _, rays_np = frame.rank_rays(cfg, rank, world, side, side * world)
     n = rays_np.shape[1]
     rays = torch.from_numpy(rays_np).to(dev)
     out_rays = torch.empty((6, n), dtype=torch.float32, device=dev)
     out_status = torch.empty(n, dtype=torch.int32, device=dev)
     out_seg = torch.empty(n, dtype=torch.int32, device=dev)
-    packed = torch.empty((8, n), dtype=torch.float32, device=dev)
+    packed = torch.empty((frame.PACKED_ROWS, n), dtype=torch.float32, device=dev)
     gather_list = [torch.empty_like(packed) for _ in range(world)] if (world > 1 and rank == 0) else None
 
     def step(ev=None):
         if ev is not None:
             ev[0].record(stream)
-        bzr_amd.trace_chain(ctx, meshes, ris, rays, out_rays, out_status, out_seg)
+        bzr_amd.trace_chain(ctx, meshes, ris, rays, out_rays, out_status, out_seg, mode=mode)
         if ev is not None:
             ev[1].record(stream)
         if world > 1 and a.gather == "step":
-            packed[:6].copy_(out_rays)
-            packed[6].copy_(out_status.view(torch.float32))
-            packed[7].copy_(out_seg.view(torch.float32))
-            dist.gather(packed, gather_list, dst=0)
+            frame.pack(out_rays, out_status, out_seg, packed)
+            frame.gather(packed, world, rank, gather_list=gather_list)
 
     for _ in range(a.warmup):
         step()
@@ -136,6 +140,8 @@ def main():
     seg_total = int(seg_total.item())
 
     events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    ctx.timing(True)
+    ctx.timing_report()  # reset
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -146,28 +152,45 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
-    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in events]))
-    t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+    kernels = ctx.timing_report()
+    ctx.timing(False)
+    chain_ms = float(np.mean([s.elapsed_time(e) for s, e in events]))
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed, kern_ms_max = float(t[0]), float(t[1])
+    elapsed = float(t[0])
 
     if rank == 0:
         ms_per_step = elapsed / a.steps * 1e3
         value = seg_total * a.steps / elapsed / 1e6
-        seg_rank0 = seg_local
         base, cnt = (None, None)
         if a.cpu_baseline == "on" and world == 1:
-            base, cnt = cpu_baseline(replace(cfg, side=side), patches, ris, a.cpu_sample_stride)
-        # algorithmic work of one k_chain launch on rank 0: planar tests + Newton candidates (oracle-measured rate)
+            base, cnt = cpu_baseline(cfg, side, patches, ris, a.cpu_sample_stride)
         if cnt and cnt["segments"]:
             newton_per_seg = (cnt["newton"] + cnt["follow"]) / cnt["segments"]
             tests_per_seg = cnt["tests"] / cnt["segments"]
-        else:
+        else:  # SURVEY.md 8d measured values for cfg2
             newton_per_seg, tests_per_seg = 1.51, float(n_patch) / len(patches)
-        flops = seg_rank0 * (FLOPS_PLANAR * tests_per_seg + FLOPS_NEWTON * newton_per_seg)
-        achieved_tflops = flops / (kern_ms * 1e-3) / 1e12
-        alg_bytes = n * (24 + 32) + n_patch * (64 + 264)
+        # algorithmic work per step on rank 0: F_seg = 33 N_b + 1750 (N_cand + N_follow)
+        seg_r0 = seg_local
+        planar_flops = seg_r0 * FLOPS_PLANAR * tests_per_seg
+        newton_flops = seg_r0 * (FLOPS_NEWTON * newton_per_seg + FLOPS_REFRACT)
+        per_kernel = {}
+        for name, (ms, calls) in kernels.items():
+            per_step = ms / a.steps
+            if name in ("k_resolve_refract", "k_resolve_hits"):
+                fl, what = newton_flops, "Newton stage + refraction of every segment (oracle-measured candidate rate)"
+            elif name == "k_traverse":
+                fl, what = planar_flops, "brute-force-equivalent planar tests (SURVEY 8d: may exceed 1 when culled)"
+            else:
+                fl, what = planar_flops + newton_flops, "brute-force segment work F_seg"
+            per_kernel[name] = {"ms_per_step": round(per_step, 4), "launches_per_step": calls / a.steps,
+                                "avg_launch_ms": round(ms / calls, 4),
+                                "alg_tflops": round(fl / (per_step * 1e-3) / 1e12, 3), "work": what}
+        dom = max(per_kernel, key=lambda k: per_kernel[k]["ms_per_step"])
+        d = per_kernel[dom]
+        achieved = d["alg_tflops"]
+        alg_bytes = n * BYTES_PER_PRIMARY
         line = {
             "metric": "Mrays/sec (primary+refracted) at 1/2/4/8 MI355X; % of HBM-read roofline",
             "value": round(value, 3),
@@ -187,23 +210,28 @@ def main():
                 "primaries_per_gpu": n,
                 "segments_per_step": seg_total,
                 "patches": n_patch,
-                "parallelism": f"image tiles x{world}" + (", RCCL gather to rank 0 each step" if world > 1 and a.gather == "step" else ""),
-                "mode": "parity (bit-identical to the oracle)",
+                "parallelism": f"image tiles x{world}" + (", RCCL gather to rank 0 in every step"
+                                                          if world > 1 and a.gather == "step" else ""),
+                "scan": "BVH-culled (bit-identical to brute force)" if a.accel == "bvh" else "brute force",
+                "numerics": "parity: bit-identical to the CPU oracle",
                 "preprocess_s": round(prep_s, 3),
+                "upload_and_bvh_s": round(upload_s, 3),
             },
             "roofline": {
                 "bound": "valu",
-                "achieved": round(achieved_tflops, 3),
+                "kernel": dom,
+                "achieved": achieved,
                 "peak": VALU_PEAK_TFLOPS,
                 "unit": "TFLOP/s",
-                "frac": round(achieved_tflops / VALU_PEAK_TFLOPS, 4),
+                "frac": round(achieved / VALU_PEAK_TFLOPS, 4),
                 "traffic": None,
-                "kernel": "k_chain",
-                "kernel_ms": round(kern_ms, 4),
-                "flops_per_launch": flops,
-                "hbm_alg_bytes_per_launch": alg_bytes,
-                "hbm_achieved_GBps": round(alg_bytes / (kern_ms * 1e-3) / 1e9, 3),
-                "hbm_frac": round(alg_bytes / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 6),
+                "avg_launch_ms": d["avg_launch_ms"],
+                "work": d["work"],
+                "per_kernel": per_kernel,
+                "chain_ms_hip_events": round(chain_ms, 4),
+                "hbm_alg_bytes_per_step": alg_bytes,
+                "hbm_achieved_GBps": round(alg_bytes / (chain_ms * 1e-3) / 1e9, 3),
+                "hbm_frac": round(alg_bytes / (chain_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 6),
                 "work_per_segment": {"planar_tests": round(tests_per_seg, 2), "newton": round(newton_per_seg, 4)},
             },
             "cpu_baseline": base,

@@ -27,11 +27,14 @@ LIB_PATH = PKG_DIR / "lib" / "libbzr.so"
 OK = 0
 HOST_PTRS, DEVICE_PTRS = 0, 1
 MODE_PARITY, MODE_FAST = 0, 2
+ACCEL_NONE = 4  # brute-force scan (A/B against the default BVH-culled path)
 WHAT_FOLLOW0, WHAT_FOLLOW1, WHAT_FOLLOW2, WHAT_NONE, WHAT_INTERSECT = 0, 1, 2, 3, 4
 LIMIT_THIS, LIMIT_NONE = 0, 1
 RR_NONE, RR_INSIDE, RR_OUTSIDE = 0, 1, 2
 ENVELOPE_ELLIPSOID, ENVELOPE_TESTLENS = 0, 1
 PATCH_WORDS = 66  # sizeof(bzr_patch) / 4
+KERNELS = ("k_traverse", "k_resolve_hits", "k_resolve_refract", "k_intersect_scan", "k_refract_scan",
+           "k_chain_scan", "k_patch")  # BZR_KERNEL_* ids
 HIT_FIELDS = 13
 
 _P = ctypes.c_void_p
@@ -50,6 +53,8 @@ _SIGS = {
     "bzr_ctx_use_own_stream": [_P],
     "bzr_ctx_get_stream": [_P, ctypes.POINTER(_P)],
     "bzr_sync": [_P],
+    "bzr_ctx_timing": [_P, _I32],
+    "bzr_ctx_timing_report": [_P, _P, _P],
     "bzr_mesh_create": [_P, _P, _U32, _U32, ctypes.POINTER(_P)],
     "bzr_mesh_destroy": [_P],
     "bzr_mesh_size": [_P, ctypes.POINTER(_U32)],
@@ -190,6 +195,17 @@ class Context:
     def sync(self):
         _check(lib().bzr_sync(self.handle))
 
+    def timing(self, enable: bool = True):
+        """Bracket every launch with hipEvents on this context's stream (bzr_ctx_timing)."""
+        _check(lib().bzr_ctx_timing(self.handle, int(bool(enable))))
+
+    def timing_report(self) -> dict:
+        """{kernel name: (total ms, launches)} since the last report (synchronises)."""
+        ms = np.zeros(len(KERNELS), np.float32)
+        calls = np.zeros(len(KERNELS), np.uint32)
+        _check(lib().bzr_ctx_timing_report(self.handle, ms.ctypes.data, calls.ctypes.data))
+        return {k: (float(ms[i]), int(calls[i])) for i, k in enumerate(KERNELS) if calls[i]}
+
     def close(self):
         if getattr(self, "handle", None):
             lib().bzr_ctx_destroy(self.handle)
@@ -242,7 +258,7 @@ def _empty_like(rays, rows, dtype):
 
 
 def intersect(ctx: Context, mesh: DeviceMesh, rays, out=None, mode=MODE_PARITY):
-    """BezierMesh::intersect over a batch -> hits [13, n]."""
+    """BezierMesh::intersect over a batch -> hits [13, n].  mode |= ACCEL_NONE for the brute-force scan."""
     n = _n_of(rays)
     out = _empty_like(rays, HIT_FIELDS, np.float32) if out is None else out
     r, o = _Buf(rays, np.float32), _Buf(out, np.float32, True)
@@ -261,7 +277,7 @@ def patch_intersect(ctx: Context, mesh: DeviceMesh, patch_index, limit, rays, ou
 
 
 def refract(ctx: Context, mesh: DeviceMesh, ri: float, rays, expected=None, expected_all=RR_INSIDE,
-            out_rays=None, out_status=None):
+            out_rays=None, out_status=None, mode=MODE_PARITY):
     """BezierLens::refract over a batch -> (rays [6, n], status [n])."""
     n = _n_of(rays)
     out_rays = _empty_like(rays, 6, np.float32) if out_rays is None else out_rays
@@ -269,11 +285,11 @@ def refract(ctx: Context, mesh: DeviceMesh, ri: float, rays, expected=None, expe
     r, e = _Buf(rays, np.float32), _Buf(expected, np.uint32)
     o, s = _Buf(out_rays, np.float32, True), _Buf(out_status, np.uint32, True)
     _check(lib().bzr_refract(ctx.handle, mesh.handle, float(ri), r.ptr, e.ptr, int(expected_all), n, o.ptr, s.ptr,
-                             _residency(r, o, s, *([e] if expected is not None else []))))
+                             _residency(r, o, s, *([e] if expected is not None else [])) | mode))
     return out_rays, out_status
 
 
-def trace_chain(ctx: Context, lenses, ri, rays, out_rays=None, out_status=None, out_segments=None):
+def trace_chain(ctx: Context, lenses, ri, rays, out_rays=None, out_status=None, out_segments=None, mode=MODE_PARITY):
     """Refraction chain through `lenses` (list of DeviceMesh) -> (rays [6, n], status [n], segments [n])."""
     n = _n_of(rays)
     nl = len(lenses)
@@ -284,7 +300,8 @@ def trace_chain(ctx: Context, lenses, ri, rays, out_rays=None, out_status=None, 
     out_segments = _empty_like(rays, 0, np.uint32) if out_segments is None else out_segments
     r = _Buf(rays, np.float32)
     o, s, g = _Buf(out_rays, np.float32, True), _Buf(out_status, np.uint32, True), _Buf(out_segments, np.uint32, True)
-    _check(lib().bzr_trace_chain(ctx.handle, handles, ris, nl, r.ptr, n, o.ptr, s.ptr, g.ptr, _residency(r, o, s, g)))
+    _check(lib().bzr_trace_chain(ctx.handle, ctypes.cast(handles, _P), ctypes.cast(ris, _P), nl, r.ptr, n, o.ptr, s.ptr,
+                                 g.ptr, _residency(r, o, s, g) | mode))
     return out_rays, out_status, out_segments
 
 

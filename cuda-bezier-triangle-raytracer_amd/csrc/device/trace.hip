@@ -1,25 +1,33 @@
 // trace.hip -- CDNA4 kernels of the hot path + the device half of the C ABI.
 //
-//   k_intersect     BezierMesh::intersect over a ray batch   (reference/bezierMesh.cpp:206-227)
-//   k_patch         BezierTriangle::intersect per (patch, ray) (reference/bezierTriangle.cpp:123-195)
-//   k_refract       BezierLens::refract                        (reference/bezierLens.cpp:4-34)
-//   k_chain         the refraction chain driver                (reference/test.cpp:376-401)
+// Reference semantics (one ray per lane, IEEE binary32, reference operation order):
+//   BezierMesh::intersect      reference/bezierMesh.cpp:206-227
+//   BezierTriangle::intersect  reference/bezierTriangle.cpp:123-195
+//   BezierLens::refract        reference/bezierLens.cpp:4-34
+//   refraction chain driver    reference/test.cpp:376-401
 //
-// One ray per lane.  The brute-force patch scan walks the mesh in index order
-// with a wave-uniform patch index, so each patch's 64-byte planar record is
-// fetched once per wave with scalar loads (s_load, SGPR operands) and shared by
-// the 64 rays of the wave; only lanes whose ray passes the planar gate run the
-// Newton stage, which loads the full 264-byte record per lane.  See DESIGN.md.
+// Two interchangeable scan strategies, identical output bits (tests/test_gpu_parity.py):
+//   culled (default)  k_traverse walks the lens BVH (bvh.cpp) wave-uniformly: node and patch
+//                     boxes are fetched with scalar loads, each lane slab-tests its own ray, the
+//                     wave descends while any lane hits (ballot), and lanes whose ray passes a
+//                     patch's exact planar gate append that patch to their candidate list.
+//                     k_resolve_* then runs the Newton stage over each ray's candidates and keeps
+//                     the (t, patch index) lexicographic minimum -- the same winner as the
+//                     reference's in-order strict-< scan.  Lists that overflow, stacks that
+//                     overflow and rays beyond the boxes' validity radius fall back to the full
+//                     in-order scan inside k_resolve_*, so every ray gets the reference result.
+//   brute force       (BZR_ACCEL_NONE) the reference's own scan: every patch's 64-byte planar
+//                     record fetched once per wave with scalar loads, Newton for passing lanes.
 #include <hip/hip_runtime.h>
 
-#include <atomic>
 #include <cstdio>
 #include <cstring>
-#include <mutex>
 #include <new>
+#include <type_traits>
 #include <string>
 #include <vector>
 
+#include "../host/bvh.hpp"
 #include "bzr.h"
 #include "patch_math.hpp"
 
@@ -32,9 +40,9 @@ bzr_status set_error(bzr_status s, const std::string &msg) {
   t_error = msg;
   return s;
 }
-#define BZR_HIP(call)                                                                                 \
-  do {                                                                                                \
-    hipError_t e_ = (call);                                                                           \
+#define BZR_HIP(call)                                                                                     \
+  do {                                                                                                    \
+    hipError_t e_ = (call);                                                                               \
     if (e_ != hipSuccess) return set_error(BZR_ERR_HIP, std::string(#call ": ") + hipGetErrorString(e_)); \
   } while (0)
 }  // namespace
@@ -45,32 +53,54 @@ extern "C" int32_t bzr_abi_version(void) { return BZR_ABI_VERSION; }
 extern "C" void bzr_internal_set_error(const char *msg) { t_error = msg ? msg : ""; }
 
 // ------------------------------------------------------------ device mesh
-// planar record (64 B) for the scan: n.xyz c | hin hout M00 M01 | M02 M10 M11 M12 | M20 M21 M22 0
 struct bzr_mesh {
   int device;
   uint32_t n;
-  float4 *planar;  // 4 float4 per patch
-  float *full;     // 66 words per patch (bzr_patch)
+  float4 *planar;   // 4 float4 per patch: n.xyz c | hin hout M00 M01 | M02 M10 M11 M12 | M20 M21 M22 0
+  float *full;      // 66 words per patch (bzr_patch)
+  bzr_host::BvhNode *nodes;
+  uint32_t *order;  // BVH leaf slots -> patch index
+  float4 *pbox;     // 2 float4 per BVH leaf slot: lo, hi of the patch's gate-region box
+  uint32_t nnodes;
+  float s_max;
 };
 
 struct bzr_ctx {
   int device;
   hipStream_t own;
   hipStream_t stream;
-  // staging buffers for host-pointer calls
-  void *scratch = nullptr;
+  void *scratch = nullptr;  // staging for host-pointer calls
   size_t scratch_bytes = 0;
+  void *work = nullptr;     // candidate lists + counts
+  size_t work_bytes = 0;
+  bool timing = false;      // per-kernel event timing (bzr_ctx_timing)
+  struct Mark {
+    int kernel;
+    hipEvent_t start, stop;
+  };
+  std::vector<Mark> marks;       // recorded, not yet reported
+  std::vector<hipEvent_t> spare; // event pool
+  double ms[BZR_KERNEL_COUNT] = {};
+  uint32_t calls[BZR_KERNEL_COUNT] = {};
 };
 
 namespace {
 
 constexpr int kBlock = 256;
+constexpr int kWaves = kBlock / 64;
 constexpr uint32_t kMaxLenses = 8;
+constexpr uint32_t kMaxCand = 8;         // candidate list length per ray and segment
+constexpr uint32_t kOverflow = 0xFFFFu;  // count value: resolve with the full scan
+constexpr int kStack = 64;
 
 struct MeshView {
   const float4 *__restrict__ planar;
   const float *__restrict__ full;
+  const bzr_host::BvhNode *__restrict__ nodes;
+  const uint32_t *__restrict__ order;
+  const float4 *__restrict__ pbox;
   uint32_t n;
+  float s_max;
   float ri;
 };
 struct LensSet {
@@ -95,6 +125,15 @@ __device__ __forceinline__ void store_hit(float *__restrict__ hits, uint32_t n, 
   reinterpret_cast<uint32_t *>(hits)[(size_t)12 * n + i] = patch;
 }
 
+__device__ __forceinline__ Hit no_hit() {
+  Hit h;
+  h.t = FLT_MAX;
+  h.what = kNone;
+  h.point = h.bary = h.normal = mk(0.0f, 0.0f, 0.0f);
+  h.cs = 0.0f;
+  return h;
+}
+
 // Planar gate of BezierTriangle::intersect with cThis (reference/bezierTriangle.cpp:124-131),
 // evaluated from the 64-byte scan record; same arithmetic as patch_intersect's first lines.
 __device__ __forceinline__ bool planar_gate(float4 q0, float4 q1, float4 q2, float4 q3, f3 s, f3 d) {
@@ -110,50 +149,84 @@ __device__ __forceinline__ bool planar_gate(float4 q0, float4 q1, float4 q2, flo
   return b0 >= 0.0f && b0 <= 1.0f && b1 >= 0.0f && b1 <= 1.0f && b2 >= 0.0f && b2 <= 1.0f;
 }
 
-// BezierMesh::intersect: brute force in index order, one follow-side retry, strict-< minimum.
-__device__ __forceinline__ Hit mesh_intersect(const MeshView &m, f3 s, f3 d, uint32_t &patch) {
-  Hit best;
-  best.t = FLT_MAX;
-  best.what = kNone;
-  best.point = best.bary = best.normal = mk(0.0f, 0.0f, 0.0f);
-  best.cs = 0.0f;
+// One iteration of the reference loop body: patch b with cThis, and on a follow-side result its
+// named neighbour with cNone (reference/bezierMesh.cpp:212-216).  `src` gets the patch that hit.
+__device__ __forceinline__ Hit evaluate_patch(const MeshView &m, uint32_t b, f3 s, f3 d, uint32_t &src) {
+  uint32_t idx = b;
+  bool limitNone = false;
+  Hit h;
+  for (int pass = 0; pass < 2; ++pass) {
+    Patch p = load_patch(m.full + (size_t)rec::kWords * idx);
+    h = patch_intersect(p, s, d, limitNone);
+    if (pass == 0 && h.what <= kFollow2) {
+      idx = __float_as_uint(m.full[(size_t)rec::kWords * idx + rec::kNeigh + h.what]);
+      limitNone = true;
+      continue;
+    }
+    break;
+  }
+  src = idx;
+  return h;
+}
+
+// BezierMesh::intersect by the reference's brute-force scan: index order, strict-< minimum.
+__device__ __forceinline__ Hit mesh_intersect_scan(const MeshView &m, f3 s, f3 d, uint32_t &patch) {
+  Hit best = no_hit();
   patch = 0xFFFFFFFFu;
   for (uint32_t b = 0; b < m.n; ++b) {
     const float4 *q = m.planar + 4u * b;  // wave-uniform address -> scalar loads
     if (!planar_gate(q[0], q[1], q[2], q[3], s, d)) continue;
-    // Newton stage for this lane; a follow-side result retries the named neighbour once with cNone
-    uint32_t idx = b;
-    bool limitNone = false;
-    Hit h;
-    for (int pass = 0; pass < 2; ++pass) {
-      Patch p = load_patch(m.full + (size_t)rec::kWords * idx);
-      h = patch_intersect(p, s, d, limitNone);
-      if (pass == 0 && h.what <= kFollow2) {
-        idx = __float_as_uint(m.full[(size_t)rec::kWords * idx + rec::kNeigh + h.what]);
-        limitNone = true;
-        continue;
-      }
-      break;
-    }
+    uint32_t src;
+    Hit h = evaluate_patch(m, b, s, d, src);
     if (h.what == kIntersect && h.t < best.t) {
       best = h;
-      patch = idx;
+      patch = src;
     }
   }
   return best;
 }
 
-// BezierLens::refract.  Returns the status; o_s/o_d = refracted ray when status != NONE.
-__device__ __forceinline__ uint32_t lens_refract(const MeshView &m, f3 s, f3 d, uint32_t expected, f3 &o_s, f3 &o_d,
-                                                 uint32_t &patch) {
-  Hit h = mesh_intersect(m, s, d, patch);
+// BezierMesh::intersect from a candidate list.  The reference keeps the first (lowest index)
+// candidate with the smallest t; over an unordered list that is the (t, index) lexicographic
+// minimum among t < FLT_MAX.  count > kMaxCand: the full in-order scan.
+__device__ __forceinline__ Hit mesh_intersect_list(const MeshView &m, f3 s, f3 d, const uint32_t *__restrict__ cand,
+                                                   uint32_t count, uint32_t n, uint32_t i, uint32_t &patch) {
+  Hit best = no_hit();
+  patch = 0xFFFFFFFFu;
+  uint32_t best_b = 0xFFFFFFFFu;
+  bool scan = count > kMaxCand;
+  uint32_t trips = scan ? m.n : count;
+  for (uint32_t j = 0; j < trips; ++j) {
+    uint32_t b;
+    if (scan) {
+      b = j;
+      const float4 *q = m.planar + 4u * b;
+      if (!planar_gate(q[0], q[1], q[2], q[3], s, d)) continue;
+    } else {
+      b = cand[(size_t)j * n + i];
+    }
+    uint32_t src;
+    Hit h = evaluate_patch(m, b, s, d, src);
+    if (h.what == kIntersect && (h.t < best.t || (h.t == best.t && best_b != 0xFFFFFFFFu && b < best_b))) {
+      best = h;
+      patch = src;
+      best_b = b;
+    }
+  }
+  return best;
+}
+
+// The refraction of BezierLens::refract after the mesh intersection.  Returns the status;
+// o_s/o_d = refracted ray when status != NONE.
+__device__ __forceinline__ uint32_t refract_hit(const Hit &h, float ri, f3 s, f3 d, uint32_t expected, f3 &o_s,
+                                                f3 &o_d) {
   o_s = s;
   o_d = d;
   uint32_t st = BZR_RR_NONE;
   if (h.what == kIntersect) {
     st = h.cs < 0.0f ? BZR_RR_INSIDE : BZR_RR_OUTSIDE;
     o_s = h.point;
-    float eta = st == BZR_RR_INSIDE ? div_rn(1.0f, m.ri) : m.ri;
+    float eta = st == BZR_RR_INSIDE ? div_rn(1.0f, ri) : ri;
     float s2 = eta * eta * (1.0f - h.cs * h.cs);
     if (s2 < 0.99f) {
       if (s2 > 1e-12f) {
@@ -183,15 +256,179 @@ __device__ __forceinline__ void store_ray(float *__restrict__ r, uint32_t n, uin
   r[(size_t)5 * n + i] = d.z;
 }
 
-__global__ __launch_bounds__(kBlock) void k_intersect(MeshView m, const float *__restrict__ rays, uint32_t n,
-                                                      float *__restrict__ hits) {
+// ------------------------------------------------------------ culled path
+__device__ __forceinline__ float safe_inv(float x) {
+  // slab test only (no parity requirement): keep 1/d finite so (b - o) * inv never makes 0 * inf
+  return 1.0f / (fabsf(x) < 1e-20f ? copysignf(1e-20f, x) : x);
+}
+
+__device__ __forceinline__ bool slab(float4 lo, float4 hi, f3 s, f3 inv) {
+  float ax = (lo.x - s.x) * inv.x, bx = (hi.x - s.x) * inv.x;
+  float ay = (lo.y - s.y) * inv.y, by = (hi.y - s.y) * inv.y;
+  float az = (lo.z - s.z) * inv.z, bz = (hi.z - s.z) * inv.z;
+  float tnear = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+  float tfar = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+  return tnear <= tfar && tfar >= 0.0f;
+}
+
+// Candidate search for one BezierMesh::intersect per active lane.  `alive` (optional): a ray is
+// traced iff alive[i] != BZR_RR_NONE.  Writes count[i] (kOverflow = resolve by full scan) and up
+// to kMaxCand patch indices cand[j*n + i].
+__global__ __launch_bounds__(kBlock) void k_traverse(MeshView m, const float *__restrict__ rays,
+                                                     const uint32_t *__restrict__ alive, uint32_t n,
+                                                     uint32_t *__restrict__ cand, uint32_t *__restrict__ count) {
+  __shared__ uint32_t stack[kWaves][kStack];
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t w = threadIdx.x >> 6;
+  bool active = i < n && (alive == nullptr || alive[i] != BZR_RR_NONE);
+  f3 s = mk(0.0f, 0.0f, 0.0f), d = s;
+  if (i < n) load_ray(rays, n, i, s, d);
+  uint32_t cnt = 0;
+  // gate-region boxes hold for ray origins within s_max (bvh.cpp); farther rays take the full scan
+  if (active && !(fmaxf(fmaxf(fabsf(s.x), fabsf(s.y)), fabsf(s.z)) <= m.s_max)) {
+    cnt = kOverflow;
+    active = false;
+  }
+  f3 inv = mk(safe_inv(d.x), safe_inv(d.y), safe_inv(d.z));
+  int sp = 0;
+  if (m.n > 0 && __any(active)) {
+    stack[w][0] = 0u;
+    sp = 1;
+  }
+  while (sp > 0) {
+    uint32_t node = __builtin_amdgcn_readfirstlane(stack[w][--sp]);
+    const bzr_host::BvhNode nd = m.nodes[node];
+    bool hit = active && slab(make_float4(nd.lo[0], nd.lo[1], nd.lo[2], 0.0f),
+                              make_float4(nd.hi[0], nd.hi[1], nd.hi[2], 0.0f), s, inv);
+    if (!__any(hit)) continue;
+    if (nd.b & bzr_host::kLeafFlag) {
+      uint32_t first = nd.a, num = nd.b & ~bzr_host::kLeafFlag;
+      for (uint32_t k = first; k < first + num; ++k) {
+        bool h2 = hit && slab(m.pbox[2 * k], m.pbox[2 * k + 1], s, inv);
+        if (!__any(h2)) continue;
+        uint32_t b = m.order[k];
+        const float4 *q = m.planar + 4u * b;
+        if (h2 && planar_gate(q[0], q[1], q[2], q[3], s, d)) {
+          if (cnt < kMaxCand) cand[(size_t)cnt * n + i] = b;
+          cnt = cnt < kMaxCand ? cnt + 1 : kOverflow;
+        }
+      }
+    } else if (sp + 2 <= kStack) {
+      stack[w][sp] = nd.b;
+      stack[w][sp + 1] = nd.a;
+      sp += 2;
+    } else {  // traversal stack exhausted: resolve these rays with the full scan
+      if (hit) cnt = kOverflow;
+    }
+  }
+  if (i < n) count[i] = cnt;
+}
+
+__global__ __launch_bounds__(kBlock) void k_resolve_hits(MeshView m, const float *__restrict__ rays,
+                                                         const uint32_t *__restrict__ cand,
+                                                         const uint32_t *__restrict__ count, uint32_t n,
+                                                         float *__restrict__ hits) {
   uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
   f3 s, d;
   load_ray(rays, n, i, s, d);
   uint32_t patch;
-  Hit h = mesh_intersect(m, s, d, patch);
+  Hit h = mesh_intersect_list(m, s, d, cand, count[i], n, i, patch);
   store_hit(hits, n, i, h, patch);
+}
+
+// One refract() per ray.  kStage == false (bzr_refract): every ray, expected from the arrays,
+// output = refracted ray or the input ray.  kStage == true (one step of the chain): only rays with
+// status[i] != NONE, rays/status updated in place, segments[i] += 1.
+template <bool kStage>
+__global__ __launch_bounds__(kBlock) void k_resolve_refract(MeshView m, const float *rays_in,
+                                                            const uint32_t *__restrict__ expected,
+                                                            uint32_t expected_all, const uint32_t *__restrict__ cand,
+                                                            const uint32_t *__restrict__ count, uint32_t n,
+                                                            float *rays_out, uint32_t *__restrict__ status,
+                                                            uint32_t *__restrict__ segments) {
+  uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  if (kStage && status[i] == BZR_RR_NONE) return;
+  f3 s, d, os, od;
+  load_ray(rays_in, n, i, s, d);
+  uint32_t patch;
+  Hit h = mesh_intersect_list(m, s, d, cand, count[i], n, i, patch);
+  uint32_t st = refract_hit(h, m.ri, s, d, expected ? expected[i] : expected_all, os, od);
+  if (st != BZR_RR_NONE || !kStage) {
+    if (st == BZR_RR_NONE) {
+      os = s;
+      od = d;
+    }
+    store_ray(rays_out, n, i, os, od);
+  }
+  status[i] = st;
+  if (kStage && segments) segments[i] += 1u;
+}
+
+__global__ void k_fill(uint32_t *__restrict__ a, uint32_t value, uint32_t n) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) a[i] = value;
+}
+
+// ------------------------------------------------------------ brute-force path
+__global__ __launch_bounds__(kBlock) void k_intersect_scan(MeshView m, const float *__restrict__ rays, uint32_t n,
+                                                           float *__restrict__ hits) {
+  uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  f3 s, d;
+  load_ray(rays, n, i, s, d);
+  uint32_t patch;
+  Hit h = mesh_intersect_scan(m, s, d, patch);
+  store_hit(hits, n, i, h, patch);
+}
+
+__global__ __launch_bounds__(kBlock) void k_refract_scan(MeshView m, const float *__restrict__ rays,
+                                                         const uint32_t *__restrict__ expected, uint32_t expected_all,
+                                                         uint32_t n, float *__restrict__ out_rays,
+                                                         uint32_t *__restrict__ out_status) {
+  uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  f3 s, d, os, od;
+  load_ray(rays, n, i, s, d);
+  uint32_t patch;
+  Hit h = mesh_intersect_scan(m, s, d, patch);
+  uint32_t st = refract_hit(h, m.ri, s, d, expected ? expected[i] : expected_all, os, od);
+  if (st == BZR_RR_NONE) {
+    os = s;
+    od = d;
+  }
+  store_ray(out_rays, n, i, os, od);
+  out_status[i] = st;
+}
+
+__global__ __launch_bounds__(kBlock) void k_chain_scan(LensSet lenses, const float *__restrict__ rays, uint32_t n,
+                                                       float *__restrict__ out_rays, uint32_t *__restrict__ out_status,
+                                                       uint32_t *__restrict__ out_segments) {
+  uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  f3 s, d;
+  load_ray(rays, n, i, s, d);
+  uint32_t st = BZR_RR_NONE, seg = 0;
+  bool alive = true;
+  for (uint32_t l = 0; l < lenses.count && alive; ++l) {
+    for (uint32_t j = 0; j < 2u && alive; ++j) {
+      f3 os, od;
+      uint32_t patch;
+      ++seg;
+      Hit h = mesh_intersect_scan(lenses.lens[l], s, d, patch);
+      st = refract_hit(h, lenses.lens[l].ri, s, d, j == 0 ? BZR_RR_INSIDE : BZR_RR_OUTSIDE, os, od);
+      if (st == BZR_RR_NONE) {
+        alive = false;
+      } else {
+        s = os;
+        d = od;
+      }
+    }
+  }
+  store_ray(out_rays, n, i, s, d);
+  out_status[i] = st;
+  if (out_segments) out_segments[i] = seg;
 }
 
 __global__ __launch_bounds__(kBlock) void k_patch(MeshView m, const uint32_t *__restrict__ idx,
@@ -207,58 +444,10 @@ __global__ __launch_bounds__(kBlock) void k_patch(MeshView m, const uint32_t *__
     Patch p = load_patch(m.full + (size_t)rec::kWords * pi);
     h = patch_intersect(p, s, d, limit[i] != 0u);
   } else {
+    h = no_hit();
     h.t = 0.0f;
-    h.point = h.bary = h.normal = mk(0.0f, 0.0f, 0.0f);
-    h.cs = 0.0f;
-    h.what = kNone;
   }
   store_hit(hits, n, i, h, pi);
-}
-
-__global__ __launch_bounds__(kBlock) void k_refract(MeshView m, const float *__restrict__ rays,
-                                                    const uint32_t *__restrict__ expected, uint32_t expected_all,
-                                                    uint32_t n, float *__restrict__ out_rays,
-                                                    uint32_t *__restrict__ out_status) {
-  uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  if (i >= n) return;
-  f3 s, d, os, od;
-  load_ray(rays, n, i, s, d);
-  uint32_t patch;
-  uint32_t st = lens_refract(m, s, d, expected ? expected[i] : expected_all, os, od, patch);
-  if (st == BZR_RR_NONE) {
-    os = s;
-    od = d;
-  }
-  store_ray(out_rays, n, i, os, od);
-  out_status[i] = st;
-}
-
-__global__ __launch_bounds__(kBlock) void k_chain(LensSet lenses, const float *__restrict__ rays, uint32_t n,
-                                                  float *__restrict__ out_rays, uint32_t *__restrict__ out_status,
-                                                  uint32_t *__restrict__ out_segments) {
-  uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  if (i >= n) return;
-  f3 s, d;
-  load_ray(rays, n, i, s, d);
-  uint32_t st = BZR_RR_NONE, seg = 0;
-  bool alive = true;
-  for (uint32_t l = 0; l < lenses.count && alive; ++l) {
-    for (uint32_t j = 0; j < 2u && alive; ++j) {
-      f3 os, od;
-      uint32_t patch;
-      ++seg;
-      st = lens_refract(lenses.lens[l], s, d, j == 0 ? BZR_RR_INSIDE : BZR_RR_OUTSIDE, os, od, patch);
-      if (st == BZR_RR_NONE) {
-        alive = false;
-      } else {
-        s = os;
-        d = od;
-      }
-    }
-  }
-  store_ray(out_rays, n, i, s, d);
-  out_status[i] = st;
-  if (out_segments) out_segments[i] = seg;
 }
 
 // ------------------------------------------------------------ host helpers
@@ -273,37 +462,78 @@ struct DeviceGuard {
   }
 };
 
-MeshView view_of(const bzr_mesh *m, float ri = 1.0f) { return MeshView{m->planar, m->full, m->n, ri}; }
+MeshView view_of(const bzr_mesh *m, float ri = 1.0f) {
+  return MeshView{m->planar, m->full, m->nodes, m->order, m->pbox, m->n, m->s_max, ri};
+}
 unsigned grid_for(uint32_t n) { return (n + kBlock - 1) / kBlock; }
+size_t round256(size_t b) { return (b + 255) & ~size_t(255); }
 
-// Host-pointer calls stage through one device allocation owned by the context.
-bzr_status ensure_scratch(bzr_ctx *ctx, size_t bytes) {
-  if (ctx->scratch_bytes >= bytes) return BZR_OK;
-  if (ctx->scratch) BZR_HIP(hipFree(ctx->scratch));
-  ctx->scratch = nullptr;
-  ctx->scratch_bytes = 0;
-  BZR_HIP(hipMalloc(&ctx->scratch, bytes));
-  ctx->scratch_bytes = bytes;
+bzr_status ensure_buffer(void *&buf, size_t &have, size_t bytes) {
+  if (have >= bytes) return BZR_OK;
+  if (buf) BZR_HIP(hipFree(buf));
+  buf = nullptr;
+  have = 0;
+  BZR_HIP(hipMalloc(&buf, bytes));
+  have = bytes;
   return BZR_OK;
 }
 
-struct Staging {  // carves device buffers out of the scratch area
+struct Staging {  // carves device buffers out of a context-owned allocation
   char *base;
   size_t off = 0;
   template <typename T>
   T *take(size_t count) {
     T *p = reinterpret_cast<T *>(base + off);
-    off += (count * sizeof(T) + 255) & ~size_t(255);
+    off += round256(count * sizeof(T));
     return p;
   }
 };
-size_t round256(size_t b) { return (b + 255) & ~size_t(255); }
 
 bzr_status check_ctx_mesh(bzr_ctx *ctx, const bzr_mesh *mesh) {
   if (!ctx) return set_error(BZR_ERR_INVALID_ARGUMENT, "null context");
   if (!mesh) return set_error(BZR_ERR_INVALID_ARGUMENT, "null mesh");
   if (mesh->device != ctx->device) return set_error(BZR_ERR_INVALID_ARGUMENT, "mesh lives on another device");
   return BZR_OK;
+}
+
+// candidate lists for n rays: kMaxCand * n + n words of the context's work area
+bzr_status work_lists(bzr_ctx *ctx, uint32_t n, uint32_t *&cand, uint32_t *&count) {
+  if (bzr_status s = ensure_buffer(ctx->work, ctx->work_bytes,
+                                   round256((size_t)kMaxCand * n * 4) + round256((size_t)n * 4)))
+    return s;
+  Staging st{static_cast<char *>(ctx->work)};
+  cand = st.take<uint32_t>((size_t)kMaxCand * n);
+  count = st.take<uint32_t>(n);
+  return BZR_OK;
+}
+
+bool use_scan(uint32_t flags) { return (flags & BZR_ACCEL_NONE) != 0; }
+
+hipEvent_t take_event(bzr_ctx *ctx) {
+  if (!ctx->spare.empty()) {
+    hipEvent_t e = ctx->spare.back();
+    ctx->spare.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  (void)hipEventCreate(&e);
+  return e;
+}
+
+// Launch on the context's stream; with timing enabled, bracket the launch with events.
+template <typename... Args>
+void launch(bzr_ctx *ctx, int kernel_id, void (*kernel)(Args...), dim3 grid, typename std::decay<Args>::type... args) {
+  hipEvent_t a = nullptr, b = nullptr;
+  if (ctx->timing) {
+    a = take_event(ctx);
+    b = take_event(ctx);
+    (void)hipEventRecord(a, ctx->stream);
+  }
+  hipLaunchKernelGGL(kernel, grid, dim3(kBlock), 0, ctx->stream, args...);
+  if (ctx->timing) {
+    (void)hipEventRecord(b, ctx->stream);
+    ctx->marks.push_back({kernel_id, a, b});
+  }
 }
 
 }  // namespace
@@ -339,12 +569,46 @@ extern "C" bzr_status bzr_ctx_create(int32_t device, bzr_ctx **out) {
   return BZR_OK;
 }
 
+extern "C" bzr_status bzr_ctx_timing(bzr_ctx *ctx, int32_t enable) {
+  if (!ctx) return set_error(BZR_ERR_INVALID_ARGUMENT, "null context");
+  ctx->timing = enable != 0;
+  return BZR_OK;
+}
+
+extern "C" bzr_status bzr_ctx_timing_report(bzr_ctx *ctx, float ms[BZR_KERNEL_COUNT], uint32_t calls[BZR_KERNEL_COUNT]) {
+  if (!ctx || !ms || !calls) return set_error(BZR_ERR_INVALID_ARGUMENT, "null argument");
+  DeviceGuard g(ctx->device);
+  BZR_HIP(hipStreamSynchronize(ctx->stream));
+  for (auto const &mk : ctx->marks) {
+    float t = 0.0f;
+    BZR_HIP(hipEventElapsedTime(&t, mk.start, mk.stop));
+    ctx->ms[mk.kernel] += t;
+    ctx->calls[mk.kernel] += 1;
+    ctx->spare.push_back(mk.start);
+    ctx->spare.push_back(mk.stop);
+  }
+  ctx->marks.clear();
+  for (int k = 0; k < BZR_KERNEL_COUNT; ++k) {
+    ms[k] = static_cast<float>(ctx->ms[k]);
+    calls[k] = ctx->calls[k];
+    ctx->ms[k] = 0.0;
+    ctx->calls[k] = 0;
+  }
+  return BZR_OK;
+}
+
 extern "C" bzr_status bzr_ctx_destroy(bzr_ctx *ctx) {
   if (!ctx) return BZR_OK;
   DeviceGuard g(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
   (void)hipStreamSynchronize(ctx->own);
+  for (auto const &mk : ctx->marks) {
+    (void)hipEventDestroy(mk.start);
+    (void)hipEventDestroy(mk.stop);
+  }
+  for (auto e : ctx->spare) (void)hipEventDestroy(e);
   if (ctx->scratch) (void)hipFree(ctx->scratch);
+  if (ctx->work) (void)hipFree(ctx->work);
   (void)hipStreamDestroy(ctx->own);
   delete ctx;
   return BZR_OK;
@@ -392,19 +656,41 @@ extern "C" bzr_status bzr_mesh_create(bzr_ctx *ctx, const void *patches, uint32_
     planar[4 * i + 2] = make_float4(m[6], m[1], m[4], m[7]);
     planar[4 * i + 3] = make_float4(m[2], m[5], m[8], 0.0f);
   }
+  bzr_host::Bvh bvh;
+  try {
+    bvh = bzr_host::build_bvh(full.data(), n, rec::kWords);
+  } catch (std::exception const &e) {
+    return set_error(BZR_ERR_OUT_OF_MEMORY, std::string("BVH build: ") + e.what());
+  }
+  if (bvh.nodes.empty()) {  // empty mesh: a root that nothing hits
+    bzr_host::BvhNode root{{1, 1, 1}, 0, {0, 0, 0}, bzr_host::kLeafFlag};
+    bvh.nodes.push_back(root);
+  }
   bzr_mesh *mesh = new (std::nothrow) bzr_mesh();
   if (!mesh) return set_error(BZR_ERR_OUT_OF_MEMORY, "mesh allocation");
   mesh->device = ctx->device;
   mesh->n = n;
-  size_t pb = planar.size() * sizeof(float4), fb = full.size() * sizeof(float);
-  hipError_t e = hipMalloc(&mesh->planar, pb ? pb : 16);
-  if (e == hipSuccess) e = hipMalloc(&mesh->full, fb ? fb : 16);
-  if (e == hipSuccess && pb) e = hipMemcpyAsync(mesh->planar, planar.data(), pb, hipMemcpyHostToDevice, ctx->stream);
-  if (e == hipSuccess && fb) e = hipMemcpyAsync(mesh->full, full.data(), fb, hipMemcpyHostToDevice, ctx->stream);
+  mesh->nnodes = static_cast<uint32_t>(bvh.nodes.size());
+  mesh->s_max = bvh.s_max;
+  struct Up {
+    void **dst;
+    const void *src;
+    size_t bytes;
+  } ups[] = {
+      {reinterpret_cast<void **>(&mesh->planar), planar.data(), planar.size() * sizeof(float4)},
+      {reinterpret_cast<void **>(&mesh->full), full.data(), full.size() * sizeof(float)},
+      {reinterpret_cast<void **>(&mesh->nodes), bvh.nodes.data(), bvh.nodes.size() * sizeof(bzr_host::BvhNode)},
+      {reinterpret_cast<void **>(&mesh->order), bvh.order.data(), bvh.order.size() * sizeof(uint32_t)},
+      {reinterpret_cast<void **>(&mesh->pbox), bvh.patch_box.data(), bvh.patch_box.size() * sizeof(float)},
+  };
+  hipError_t e = hipSuccess;
+  for (auto &u : ups) {
+    if (e == hipSuccess) e = hipMalloc(u.dst, u.bytes ? u.bytes : 16);
+    if (e == hipSuccess && u.bytes) e = hipMemcpyAsync(*u.dst, u.src, u.bytes, hipMemcpyHostToDevice, ctx->stream);
+  }
   if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
   if (e != hipSuccess) {
-    (void)hipFree(mesh->planar);
-    (void)hipFree(mesh->full);
+    for (auto &u : ups) (void)hipFree(*u.dst);
     delete mesh;
     return set_error(BZR_ERR_HIP, std::string("mesh upload: ") + hipGetErrorString(e));
   }
@@ -418,6 +704,9 @@ extern "C" bzr_status bzr_mesh_destroy(bzr_mesh *mesh) {
   (void)hipDeviceSynchronize();
   (void)hipFree(mesh->planar);
   (void)hipFree(mesh->full);
+  (void)hipFree(mesh->nodes);
+  (void)hipFree(mesh->order);
+  (void)hipFree(mesh->pbox);
   delete mesh;
   return BZR_OK;
 }
@@ -439,14 +728,24 @@ extern "C" bzr_status bzr_intersect(bzr_ctx *ctx, const bzr_mesh *mesh, const fl
   bool host = !(flags & BZR_DEVICE_PTRS);
   if (host) {
     size_t rb = (size_t)n * 6 * sizeof(float), hb = (size_t)n * 13 * sizeof(float);
-    if (bzr_status s = ensure_scratch(ctx, round256(rb) + round256(hb))) return s;
+    if (bzr_status s = ensure_buffer(ctx->scratch, ctx->scratch_bytes, round256(rb) + round256(hb))) return s;
     Staging st{static_cast<char *>(ctx->scratch)};
     float *r = st.take<float>((size_t)n * 6);
     d_hits = st.take<float>((size_t)n * 13);
     BZR_HIP(hipMemcpyAsync(r, rays, rb, hipMemcpyHostToDevice, ctx->stream));
     d_rays = r;
   }
-  hipLaunchKernelGGL(k_intersect, dim3(grid_for(n)), dim3(kBlock), 0, ctx->stream, view_of(mesh), d_rays, n, d_hits);
+  MeshView mv = view_of(mesh);
+  if (use_scan(flags)) {
+    launch(ctx, BZR_KERNEL_INTERSECT_SCAN, k_intersect_scan, dim3(grid_for(n)), mv, d_rays, n, d_hits);
+  } else {
+    uint32_t *cand, *count;
+    if (bzr_status s = work_lists(ctx, n, cand, count)) return s;
+    launch(ctx, BZR_KERNEL_TRAVERSE, k_traverse, dim3(grid_for(n)), mv, d_rays,
+                       static_cast<const uint32_t *>(nullptr), n, cand, count);
+    launch(ctx, BZR_KERNEL_RESOLVE_HITS, k_resolve_hits, dim3(grid_for(n)), mv, d_rays, cand, count, n,
+                       d_hits);
+  }
   BZR_HIP(hipGetLastError());
   if (host) {
     BZR_HIP(hipMemcpyAsync(hits, d_hits, (size_t)n * 13 * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
@@ -467,7 +766,8 @@ extern "C" bzr_status bzr_patch_intersect(bzr_ctx *ctx, const bzr_mesh *mesh, co
   bool host = !(flags & BZR_DEVICE_PTRS);
   if (host) {
     size_t ib = (size_t)n * 4, rb = (size_t)n * 24, hb = (size_t)n * 52;
-    if (bzr_status s = ensure_scratch(ctx, 2 * round256(ib) + round256(rb) + round256(hb))) return s;
+    if (bzr_status s = ensure_buffer(ctx->scratch, ctx->scratch_bytes, 2 * round256(ib) + round256(rb) + round256(hb)))
+      return s;
     Staging st{static_cast<char *>(ctx->scratch)};
     uint32_t *a = st.take<uint32_t>(n), *b = st.take<uint32_t>(n);
     float *r = st.take<float>((size_t)n * 6);
@@ -479,7 +779,7 @@ extern "C" bzr_status bzr_patch_intersect(bzr_ctx *ctx, const bzr_mesh *mesh, co
     d_lim = b;
     d_rays = r;
   }
-  hipLaunchKernelGGL(k_patch, dim3(grid_for(n)), dim3(kBlock), 0, ctx->stream, view_of(mesh), d_idx, d_lim, d_rays, n,
+  launch(ctx, BZR_KERNEL_PATCH, k_patch, dim3(grid_for(n)), view_of(mesh), d_idx, d_lim, d_rays, n,
                      d_hits);
   BZR_HIP(hipGetLastError());
   if (host) {
@@ -503,7 +803,7 @@ extern "C" bzr_status bzr_refract(bzr_ctx *ctx, const bzr_mesh *mesh, float ri, 
   bool host = !(flags & BZR_DEVICE_PTRS);
   if (host) {
     size_t rb = (size_t)n * 24, ib = (size_t)n * 4;
-    if (bzr_status s = ensure_scratch(ctx, 2 * round256(rb) + 2 * round256(ib))) return s;
+    if (bzr_status s = ensure_buffer(ctx->scratch, ctx->scratch_bytes, 2 * round256(rb) + 2 * round256(ib))) return s;
     Staging st{static_cast<char *>(ctx->scratch)};
     float *r = st.take<float>((size_t)n * 6);
     uint32_t *e = st.take<uint32_t>(n);
@@ -514,8 +814,18 @@ extern "C" bzr_status bzr_refract(bzr_ctx *ctx, const bzr_mesh *mesh, float ri, 
     d_rays = r;
     d_exp = expected ? e : nullptr;
   }
-  hipLaunchKernelGGL(k_refract, dim3(grid_for(n)), dim3(kBlock), 0, ctx->stream, view_of(mesh, ri), d_rays, d_exp,
-                     expected_all, n, d_out, d_st);
+  MeshView mv = view_of(mesh, ri);
+  if (use_scan(flags)) {
+    launch(ctx, BZR_KERNEL_REFRACT_SCAN, k_refract_scan, dim3(grid_for(n)), mv, d_rays, d_exp, expected_all,
+                       n, d_out, d_st);
+  } else {
+    uint32_t *cand, *count;
+    if (bzr_status s = work_lists(ctx, n, cand, count)) return s;
+    launch(ctx, BZR_KERNEL_TRAVERSE, k_traverse, dim3(grid_for(n)), mv, d_rays,
+                       static_cast<const uint32_t *>(nullptr), n, cand, count);
+    launch(ctx, BZR_KERNEL_RESOLVE_REFRACT, k_resolve_refract<false>, dim3(grid_for(n)), mv, d_rays, d_exp,
+                       expected_all, cand, count, n, d_out, d_st, static_cast<uint32_t *>(nullptr));
+  }
   BZR_HIP(hipGetLastError());
   if (host) {
     BZR_HIP(hipMemcpyAsync(out_rays, d_out, (size_t)n * 24, hipMemcpyDeviceToHost, ctx->stream));
@@ -539,6 +849,7 @@ extern "C" bzr_status bzr_trace_chain(bzr_ctx *ctx, const bzr_mesh *const *lense
   }
   if (n == 0) return BZR_OK;
   if (!rays || !out_rays || !out_status) return set_error(BZR_ERR_INVALID_ARGUMENT, "null buffer");
+  if (rays == out_rays) return set_error(BZR_ERR_INVALID_ARGUMENT, "rays and out_rays must not alias");
   DeviceGuard g(ctx->device);
   const float *d_rays = rays;
   float *d_out = out_rays;
@@ -546,17 +857,37 @@ extern "C" bzr_status bzr_trace_chain(bzr_ctx *ctx, const bzr_mesh *const *lense
   bool host = !(flags & BZR_DEVICE_PTRS);
   if (host) {
     size_t rb = (size_t)n * 24, ib = (size_t)n * 4;
-    if (bzr_status s = ensure_scratch(ctx, 2 * round256(rb) + 2 * round256(ib))) return s;
+    if (bzr_status s = ensure_buffer(ctx->scratch, ctx->scratch_bytes, 2 * round256(rb) + 2 * round256(ib))) return s;
     Staging st{static_cast<char *>(ctx->scratch)};
     float *r = st.take<float>((size_t)n * 6);
     d_out = st.take<float>((size_t)n * 6);
     d_st = st.take<uint32_t>(n);
-    d_seg = out_segments ? st.take<uint32_t>(n) : nullptr;
+    d_seg = st.take<uint32_t>(n);
     BZR_HIP(hipMemcpyAsync(r, rays, rb, hipMemcpyHostToDevice, ctx->stream));
     d_rays = r;
   }
-  hipLaunchKernelGGL(k_chain, dim3(grid_for(n)), dim3(kBlock), 0, ctx->stream, set, d_rays, n, d_out, d_st, d_seg);
-  BZR_HIP(hipGetLastError());
+  if (use_scan(flags)) {
+    launch(ctx, BZR_KERNEL_CHAIN_SCAN, k_chain_scan, dim3(grid_for(n)), set, d_rays, n, d_out, d_st, d_seg);
+    BZR_HIP(hipGetLastError());
+  } else {
+    // stage by stage: out_rays holds the rays in flight, out_status != NONE marks them alive
+    uint32_t *cand, *count;
+    if (bzr_status s = work_lists(ctx, n, cand, count)) return s;
+    BZR_HIP(hipMemcpyAsync(d_out, d_rays, (size_t)n * 24, hipMemcpyDeviceToDevice, ctx->stream));
+    hipLaunchKernelGGL(k_fill, dim3(grid_for(n)), dim3(kBlock), 0, ctx->stream, d_st, uint32_t(BZR_RR_INSIDE), n);
+    if (d_seg) hipLaunchKernelGGL(k_fill, dim3(grid_for(n)), dim3(kBlock), 0, ctx->stream, d_seg, 0u, n);
+    for (uint32_t l = 0; l < nlens; ++l) {
+      for (uint32_t j = 0; j < 2; ++j) {
+        launch(ctx, BZR_KERNEL_TRAVERSE, k_traverse, dim3(grid_for(n)), set.lens[l], d_out, d_st, n,
+                           cand, count);
+        launch(ctx, BZR_KERNEL_RESOLVE_REFRACT, k_resolve_refract<true>, dim3(grid_for(n)), set.lens[l], d_out,
+                           static_cast<const uint32_t *>(nullptr),
+                           j == 0 ? uint32_t(BZR_RR_INSIDE) : uint32_t(BZR_RR_OUTSIDE), cand, count, n, d_out, d_st,
+                           d_seg);
+      }
+    }
+    BZR_HIP(hipGetLastError());
+  }
   if (host) {
     BZR_HIP(hipMemcpyAsync(out_rays, d_out, (size_t)n * 24, hipMemcpyDeviceToHost, ctx->stream));
     BZR_HIP(hipMemcpyAsync(out_status, d_st, (size_t)n * 4, hipMemcpyDeviceToHost, ctx->stream));

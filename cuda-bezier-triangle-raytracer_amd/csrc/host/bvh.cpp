@@ -1,0 +1,244 @@
+// bvh.cpp -- exact-preserving culling structure for one lens mesh (host build, device use).
+//
+// BezierMesh::intersect (reference/bezierMesh.cpp:206-227) scans every patch.  A patch can
+// only contribute when its planar gate passes (reference/bezierTriangle.cpp:124-131): the
+// ray/plane point p satisfies 0 <= M p <= 1 componentwise (M = mBarycentricInverse).  That set,
+// intersected with the underlying plane, is a convex polygon -- usually the flat triangle
+// (cp0, cp1, cp2), but much larger when the plane passes near the origin and M is
+// ill-conditioned, so it is computed here in double precision by clipping the
+// plane against the six half-spaces of M's rows, loosened by the rounding slack of the float
+// gate.  Its inflated AABB is the patch's culling box; a median-split BVH over those boxes is
+// traversed on the GPU.  A ray that misses a box cannot pass that patch's gate, so the set of
+// patches that reach the Newton stage -- and therefore every output bit -- is the brute-force
+// scan's.  The per-ray part of the slack (ray origin magnitude) is added on the device.
+#include "bvh.hpp"
+
+#include <algorithm>
+#include <array>
+#include <cmath>
+#include <cstring>
+#include <numeric>
+
+namespace bzr_host {
+namespace {
+
+using d3 = std::array<double, 3>;
+d3 sub(d3 a, d3 b) { return {a[0] - b[0], a[1] - b[1], a[2] - b[2]}; }
+d3 addm(d3 a, d3 b, double s) { return {a[0] + s * b[0], a[1] + s * b[1], a[2] + s * b[2]}; }
+double dotd(d3 a, d3 b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+d3 crossd(d3 a, d3 b) { return {a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]}; }
+double normd(d3 a) { return std::sqrt(dotd(a, a)); }
+
+constexpr double kRel = 1.0 / (1 << 18);  // rounding slack factor (~32x the float gate's unit error)
+
+// Clip convex polygon `poly` (plane points) to { x : g.x + h >= 0 }.
+std::vector<d3> clip(std::vector<d3> const &poly, d3 g, double h) {
+  std::vector<d3> out;
+  std::size_t m = poly.size();
+  for (std::size_t i = 0; i < m; ++i) {
+    d3 a = poly[i], b = poly[(i + 1) % m];
+    double fa = dotd(g, a) + h, fb = dotd(g, b) + h;
+    if (fa >= 0) out.push_back(a);
+    if ((fa >= 0) != (fb >= 0)) {
+      double t = fa / (fa - fb);
+      out.push_back(addm(a, sub(b, a), t));
+    }
+  }
+  return out;
+}
+
+// Conservative AABB of the region where the float planar gate of one patch can pass, for rays whose
+// origin satisfies |s|_inf <= s_max.  The gate accepts p when 0 <= fl(M p) <= 1; p is the float
+// ray/plane point, within eps of the plane and within pad of the ray.  So the region is the
+// parallelepiped P = { x : -slack <= M_i x <= 1 + slack } cut by the slab |n.x - c| <= eps:
+// its AABB is spanned by the two slab-face slices of P and the vertices of P inside the slab.
+Box gate_region_box(const float *rec, double s_max) {
+  d3 n{rec[0], rec[1], rec[2]};
+  double c = rec[3];
+  const float *m = rec + 49;  // col-major
+  d3 row[3];
+  for (int i = 0; i < 3; ++i) row[i] = {m[i], m[3 + i], m[6 + i]};
+  Box all;
+  all.lo = {-HUGE_VALF, -HUGE_VALF, -HUGE_VALF};
+  all.hi = {HUGE_VALF, HUGE_VALF, HUGE_VALF};
+  double nn = normd(n);
+  if (!(nn > 0) || !std::isfinite(c)) return all;
+  for (auto const &r : row)
+    if (!std::isfinite(r[0]) || !std::isfinite(r[1]) || !std::isfinite(r[2])) return all;
+  d3 nu = {n[0] / nn, n[1] / nn, n[2] / nn};
+  double cu = c / nn;
+  d3 helper = std::fabs(nu[0]) < 0.6 ? d3{1, 0, 0} : (std::fabs(nu[1]) < 0.6 ? d3{0, 1, 0} : d3{0, 0, 1});
+  d3 u = crossd(nu, helper);
+  double un = normd(u);
+  u = {u[0] / un, u[1] / un, u[2] / un};
+  d3 v = crossd(nu, u);
+  // Q = M^-1 (double): P's vertices are Q b, b in {-slack, 1+slack}^3
+  double md[9];
+  for (int i = 0; i < 9; ++i) md[i] = m[i];
+  auto at = [&md](int i, int j) { return md[j * 3 + i]; };
+  double det = at(0, 0) * (at(1, 1) * at(2, 2) - at(1, 2) * at(2, 1)) - at(0, 1) * (at(1, 0) * at(2, 2) - at(1, 2) * at(2, 0)) +
+               at(0, 2) * (at(1, 0) * at(2, 1) - at(1, 1) * at(2, 0));
+  if (!(std::fabs(det) > 0) || !std::isfinite(det)) return all;
+  d3 q[3];
+  double ext = std::fabs(cu) + 1.0;
+  for (int k = 0; k < 3; ++k) {  // column k of M^-1: inv(i,k) = cof(k,i) / det
+    for (int i = 0; i < 3; ++i) {
+      int r1 = (k + 1) % 3, r2 = (k + 2) % 3, c1 = (i + 1) % 3, c2 = (i + 2) % 3;
+      q[k][i] = (at(r1, c1) * at(r2, c2) - at(r1, c2) * at(r2, c1)) / det;
+    }
+    ext += 2.0 * normd(q[k]);
+  }
+  if (!std::isfinite(ext)) return all;
+  double X = ext;  // bound on |x| over P (every vertex of P is within sum |q_k| (1 + 2 slack))
+  double slack[3];
+  for (int i = 0; i < 3; ++i) {
+    double l1 = std::fabs(row[i][0]) + std::fabs(row[i][1]) + std::fabs(row[i][2]);
+    slack[i] = kRel * (l1 * X + 1.0);
+  }
+  double eps = kRel * (X + s_max);  // off-plane distance of the float plane point
+  d3 lo{HUGE_VAL, HUGE_VAL, HUGE_VAL}, hi{-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
+  bool any = false;
+  auto take = [&](d3 const &p) {
+    any = true;
+    for (int a = 0; a < 3; ++a) {
+      lo[a] = std::min(lo[a], p[a]);
+      hi[a] = std::max(hi[a], p[a]);
+    }
+  };
+  for (double off : {-eps, eps}) {
+    d3 x0 = {nu[0] * (cu + off), nu[1] * (cu + off), nu[2] * (cu + off)};
+    double e = 2.0 * (ext + std::fabs(cu) + eps);
+    std::vector<d3> region = {addm(addm(x0, u, -e), v, -e), addm(addm(x0, u, e), v, -e),
+                              addm(addm(x0, u, e), v, e), addm(addm(x0, u, -e), v, e)};
+    for (int i = 0; i < 3 && !region.empty(); ++i) {
+      region = clip(region, row[i], slack[i]);                                                   // M_i x >= -slack
+      if (!region.empty()) region = clip(region, {-row[i][0], -row[i][1], -row[i][2]}, 1.0 + slack[i]);  // <= 1+slack
+    }
+    for (auto const &p : region) take(p);
+  }
+  for (int corner = 0; corner < 8; ++corner) {
+    d3 b;
+    for (int k = 0; k < 3; ++k) b[k] = (corner >> k) & 1 ? 1.0 + slack[k] : -slack[k];
+    d3 p{0, 0, 0};
+    for (int k = 0; k < 3; ++k) p = addm(p, q[k], b[k]);
+    if (std::fabs(dotd(nu, p) - cu) <= eps) take(p);
+  }
+  Box bx;
+  if (!any) {  // no point of the slab passes the gate even with slack: never a candidate
+    bx.lo = {1.0f, 1.0f, 1.0f};
+    bx.hi = {0.0f, 0.0f, 0.0f};
+    bx.empty = true;
+    return bx;
+  }
+  double pad = kRel * (X + s_max) + 1e-6;  // ray-point and slab-test rounding
+  for (int a = 0; a < 3; ++a) {
+    bx.lo[a] = static_cast<float>(std::nextafter(lo[a] - pad, -HUGE_VAL));
+    bx.hi[a] = static_cast<float>(std::nextafter(hi[a] + pad, HUGE_VAL));
+  }
+  return bx;
+}
+
+struct Builder {
+  std::vector<Box> const &box;
+  std::vector<std::array<float, 3>> centre;
+  std::vector<uint32_t> &order;
+  std::vector<BvhNode> &nodes;
+
+  uint32_t build(uint32_t first, uint32_t count) {
+    uint32_t id = static_cast<uint32_t>(nodes.size());
+    nodes.push_back({});
+    Box bb;
+    bb.lo = {HUGE_VALF, HUGE_VALF, HUGE_VALF};
+    bb.hi = {-HUGE_VALF, -HUGE_VALF, -HUGE_VALF};
+    std::array<float, 3> clo{HUGE_VALF, HUGE_VALF, HUGE_VALF}, chi{-HUGE_VALF, -HUGE_VALF, -HUGE_VALF};
+    for (uint32_t k = first; k < first + count; ++k) {
+      Box const &b = box[order[k]];
+      for (int a = 0; a < 3; ++a) {
+        if (!b.empty) {
+          bb.lo[a] = std::min(bb.lo[a], b.lo[a]);
+          bb.hi[a] = std::max(bb.hi[a], b.hi[a]);
+        }
+        clo[a] = std::min(clo[a], centre[order[k]][a]);
+        chi[a] = std::max(chi[a], centre[order[k]][a]);
+      }
+    }
+    BvhNode nd;
+    std::memcpy(nd.lo, bb.lo.data(), 12);
+    std::memcpy(nd.hi, bb.hi.data(), 12);
+    if (count <= kLeafSize) {
+      nd.a = first;
+      nd.b = kLeafFlag | count;
+      nodes[id] = nd;
+      return id;
+    }
+    int axis = 0;
+    for (int a = 1; a < 3; ++a)
+      if (chi[a] - clo[a] > chi[axis] - clo[axis]) axis = a;
+    uint32_t half = count / 2;
+    std::nth_element(order.begin() + first, order.begin() + first + half, order.begin() + first + count,
+                     [&](uint32_t x, uint32_t y) {
+                       return centre[x][axis] < centre[y][axis] || (centre[x][axis] == centre[y][axis] && x < y);
+                     });
+    uint32_t left = build(first, half);
+    uint32_t right = build(first + half, count - half);
+    nd.a = left;
+    nd.b = right;
+    nodes[id] = nd;
+    return id;
+  }
+};
+
+}  // namespace
+
+Bvh build_bvh(const float *records, uint32_t n, uint32_t stride_words) {
+  Bvh out;
+  std::vector<Box> box(n);
+  Builder bld{box, std::vector<std::array<float, 3>>(n), out.order, out.nodes};
+  // ray origins up to s_max (100x the mesh's control-point extent, at least 1e3) use the culled
+  // path; farther origins are routed to the brute-force scan by the kernel.
+  double span = 0.0;
+  for (uint32_t i = 0; i < n; ++i)
+    for (int k = 0; k < 30; ++k) {
+      double x = std::fabs(records[(size_t)i * stride_words + 19 + k]);
+      if (std::isfinite(x)) span = std::max(span, x);
+    }
+  out.s_max = static_cast<float>(std::max(1e3, 100.0 * span));
+  out.extent = 0.0f;
+  for (uint32_t i = 0; i < n; ++i) {
+    box[i] = gate_region_box(records + (size_t)i * stride_words, out.s_max);
+    for (int a = 0; a < 3; ++a) {
+      float lo = box[i].lo[a], hi = box[i].hi[a];
+      bld.centre[i][a] = box[i].empty ? 0.0f : (std::isfinite(lo) && std::isfinite(hi) ? 0.5f * (lo + hi) : 0.0f);
+      if (!box[i].empty) out.extent = std::max({out.extent, std::fabs(lo), std::fabs(hi)});
+    }
+  }
+  if (!std::isfinite(out.extent)) out.extent = HUGE_VALF;
+  out.order.resize(n);
+  std::iota(out.order.begin(), out.order.end(), 0u);
+  if (n) bld.build(0, n);
+  out.patch_box.resize((size_t)n * 8);
+  for (uint32_t k = 0; k < n; ++k) {
+    Box const &b = box[out.order[k]];
+    float *d = &out.patch_box[(size_t)k * 8];
+    d[0] = b.lo[0]; d[1] = b.lo[1]; d[2] = b.lo[2]; d[3] = 0.0f;
+    d[4] = b.hi[0]; d[5] = b.hi[1]; d[6] = b.hi[2]; d[7] = 0.0f;
+  }
+  return out;
+}
+
+}  // namespace bzr_host
+
+// ---- debug / test entry point (include/bzr_debug.h) ----
+extern "C" int32_t bzr_debug_gate_boxes(const void *patches, uint32_t n, uint32_t stride, float *boxes, float *s_max) {
+  if ((!patches && n) || (!boxes && n) || !s_max || stride % 4 || stride < 264) return 1;
+  bzr_host::Bvh bvh = bzr_host::build_bvh(static_cast<const float *>(patches), n, stride / 4);
+  for (uint32_t k = 0; k < n; ++k) {
+    uint32_t p = bvh.order[k];
+    for (int a = 0; a < 3; ++a) {
+      boxes[(size_t)p * 6 + a] = bvh.patch_box[(size_t)k * 8 + a];
+      boxes[(size_t)p * 6 + 3 + a] = bvh.patch_box[(size_t)k * 8 + 4 + a];
+    }
+  }
+  *s_max = bvh.s_max;
+  return 0;
+}

@@ -29,9 +29,13 @@
  *   - Pointer residency is selected per call by BZR_DEVICE_PTRS; host-pointer
  *     calls are synchronous, device-pointer calls are asynchronous on the
  *     context's stream until bzr_sync().
- *   - Numerics: BZR_MODE_PARITY (default) evaluates in IEEE binary32 with the
- *     reference's operation order and no contraction, bit-identical to the
- *     CPU oracle.  BZR_MODE_FAST allows FMA contraction in the Newton stage.
+ *   - Numerics: IEEE binary32 with the reference's operation order and no
+ *     contraction, bit-identical to the CPU oracle (BZR_MODE_PARITY, the only
+ *     mode implemented; BZR_MODE_FAST is reserved).
+ *   - Scan strategy: by default each lens mesh carries a BVH over the regions
+ *     where each patch's planar gate can pass, and only those patches reach
+ *     the Newton stage -- the output bits are the brute-force scan's.
+ *     BZR_ACCEL_NONE runs the reference's brute-force scan itself (A/B testing).
  */
 #ifndef BZR_H
 #define BZR_H
@@ -59,7 +63,8 @@ enum {
   BZR_HOST_PTRS = 0u,
   BZR_DEVICE_PTRS = 1u,
   BZR_MODE_PARITY = 0u,
-  BZR_MODE_FAST = 2u
+  BZR_MODE_FAST = 2u,
+  BZR_ACCEL_NONE = 4u   /* brute-force patch scan instead of the (bit-identical) BVH-culled path */
 };
 
 enum { BZR_WHAT_FOLLOW0 = 0, BZR_WHAT_FOLLOW1 = 1, BZR_WHAT_FOLLOW2 = 2, BZR_WHAT_NONE = 3, BZR_WHAT_INTERSECT = 4 };
@@ -97,6 +102,23 @@ bzr_status bzr_ctx_set_stream(bzr_ctx *ctx, void *hip_stream);
 bzr_status bzr_ctx_use_own_stream(bzr_ctx *ctx);
 bzr_status bzr_ctx_get_stream(bzr_ctx *ctx, void **hip_stream);
 bzr_status bzr_sync(bzr_ctx *ctx);
+
+/* ---- measurement: per-kernel HIP-event timing on the context's stream ---- */
+enum {
+  BZR_KERNEL_TRAVERSE = 0,        /* BVH candidate search */
+  BZR_KERNEL_RESOLVE_HITS = 1,    /* Newton stage -> BezierIntersection */
+  BZR_KERNEL_RESOLVE_REFRACT = 2, /* Newton stage + refraction */
+  BZR_KERNEL_INTERSECT_SCAN = 3,  /* brute force (BZR_ACCEL_NONE) */
+  BZR_KERNEL_REFRACT_SCAN = 4,
+  BZR_KERNEL_CHAIN_SCAN = 5,
+  BZR_KERNEL_PATCH = 6,
+  BZR_KERNEL_COUNT = 7
+};
+/* While enabled, every launch is bracketed by hipEvents on the context's stream. */
+bzr_status bzr_ctx_timing(bzr_ctx *ctx, int32_t enable);
+/* Synchronises, returns the summed milliseconds and launch counts per kernel id since the last
+ * report, and resets them. */
+bzr_status bzr_ctx_timing_report(bzr_ctx *ctx, float ms[BZR_KERNEL_COUNT], uint32_t calls[BZR_KERNEL_COUNT]);
 
 /* ---- device mesh: BezierMesh's patch vector (reference/bezierMesh.h:17) ---- */
 /* Copies n records of `stride` bytes (stride >= sizeof(bzr_patch)) from host memory. */

@@ -19,6 +19,7 @@
 #endif
 
 static char g_err[256];
+
 const char *orc_last_error(void) { return g_err; }
 static int fail(const char *msg) { snprintf(g_err, sizeof g_err, "%s", msg); return -1; }
 
@@ -1295,6 +1296,16 @@ void orc_trace_chain_batch(const opatch *const *lp, const uint32_t *lnp, const f
     ray_to_soa(out_rays, n, i, &r);
     out_status[i] = st;
     out_seg[i] = seg;
+  }
+}
+
+/* the planar gate matrix: out[r * np + i] = 1 iff ray r passes patch i's gate (cThis) */
+void orc_planar_gate_batch(const opatch *p, uint32_t np, const float *rays, uint32_t n, uint8_t *out, int threads) {
+  set_threads(threads);
+#pragma omp parallel for schedule(dynamic, 16)
+  for (int64_t rr = 0; rr < (int64_t)n; ++rr) {
+    oray r = ray_from_soa(rays, n, (uint32_t)rr);
+    for (uint32_t i = 0; i < np; ++i) out[(size_t)rr * np + i] = (uint8_t)planar_candidate(&p[i], &r);
   }
 }
 

@@ -143,6 +143,8 @@ void     orc_trace_chain_batch(const opatch *const *lens_patches, const uint32_t
 void     orc_refract_batch(const opatch *p, uint32_t np, float ri, const float *rays_soa, const uint32_t *expected,
                            uint32_t n, float *out_rays_soa, uint32_t *out_status, int threads);
 
+/* test hook: out[r * np + i] = 1 iff ray r passes patch i's planar gate (cThis) */
+void     orc_planar_gate_batch(const opatch *p, uint32_t np, const float *rays_soa, uint32_t n, uint8_t *out, int threads);
 /* work counters since the last reset: planar tests, Newton runs, follow-side retries, intersect calls */
 void     orc_counters(uint64_t out[4]);
 void     orc_counters_reset(void);

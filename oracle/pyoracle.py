@@ -87,6 +87,7 @@ def lib():
                                            ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
             "orc_debug_uset_order": ([_P, ctypes.c_uint32, _P], ctypes.c_uint32),
             "orc_counters": ([_P], None),
+            "orc_planar_gate_batch": ([_P, ctypes.c_uint32, _P, ctypes.c_uint32, _P, ctypes.c_int], None),
             "orc_counters_reset": ([], None),
             "orc_plane_from_1proportion_2points": ([ctypes.c_float, ov3, ov3], oplane),
             "orc_plane_from_3points": ([ov3, ov3, ov3], oplane),
@@ -288,6 +289,15 @@ def trace_chain(lenses, ri, rays, threads=0):
                                 ctypes.cast(ris, ctypes.c_void_p), len(ps), r.ctypes.data, n, o.ctypes.data,
                                 s.ctypes.data, g.ctypes.data, threads)
     return o, s, g
+
+
+def planar_gate(patches, rays, threads=0) -> np.ndarray:
+    """bool [n_rays, n_patches]: the planar gate of BezierTriangle::intersect (reference/bezierTriangle.cpp:124-131)."""
+    p = np.ascontiguousarray(patches, dtype=np.float32)
+    r = np.ascontiguousarray(rays, dtype=np.float32)
+    out = np.zeros((r.shape[1], len(p)), np.uint8)
+    lib().orc_planar_gate_batch(p.ctypes.data, len(p), r.ctypes.data, r.shape[1], out.ctypes.data, threads)
+    return out.astype(bool)
 
 
 def counters_reset():

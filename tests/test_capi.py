@@ -1,0 +1,65 @@
+"""The C-ABI library: it loads without a GPU, exports every symbol include/*.h declares, reports
+errors as status codes + text, and refuses to run the hot path without a HIP device (no CPU fallback)."""
+import ctypes
+import re
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+REPO = Path(__file__).resolve().parents[1]
+
+
+def declared(header):
+    text = (REPO / "include" / header).read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(bzr_[a-z0-9_]+)\s*\(", text)))
+
+
+@pytest.mark.parametrize("header", ["bzr.h", "bzr_debug.h"])
+def test_every_declared_symbol_is_exported(bzr, header):
+    lib = ctypes.CDLL(str(bzr.LIB_PATH))
+    names = declared(header)
+    assert len(names) > (30 if header == "bzr.h" else 0)
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+
+
+def test_python_binding_covers_the_header(bzr):
+    assert set(declared("bzr.h")) <= set(bzr.exported_symbols())
+
+
+def test_abi_version_and_patch_layout(bzr):
+    assert bzr.lib().bzr_abi_version() == 1
+    # bzr_patch is the reference's 264-byte BezierTriangle (reference/bezierTriangle.h:64-80)
+    assert bzr.PATCH_WORDS * 4 == 264
+
+
+def test_hot_path_needs_a_device(bzr):
+    if bzr.device_count() > 0:
+        pytest.skip("a GPU is visible here")
+    with pytest.raises(bzr.BzrError, match="no HIP device"):
+        bzr.Context(0)
+
+
+def test_errors_are_status_codes(bzr):
+    L = bzr.lib()
+    assert L.bzr_trimesh_split(None, 2) == 1
+    assert b"null" in L.bzr_last_error()
+    m = bzr.TriMesh()
+    with pytest.raises(bzr.BzrError, match="divisor"):
+        m.split(0)
+    with pytest.raises(bzr.BzrError, match="cannot open"):
+        m.read_stl("/nonexistent/file.stl")
+    with pytest.raises(bzr.BzrError, match="not standardized"):
+        bzr.TriMesh().make_ellipsoid(4, 2).bezier_patches()
+
+
+def test_patch_records_view_as_reference_struct(bzr):
+    """The 66-word records reinterpret as the bzr_patch / BezierTriangle layout: neighbours are u32 indices
+    into the patch array, the direction vector A is (1, 0, -1) (reference/bezierTriangle.cpp:83)."""
+    p = bzr.TriMesh().make_unit_sphere(3, 7).standardize().bezier_patches()
+    neigh = p[:, 16:19].view(np.uint32)
+    assert neigh.max() < len(p)
+    assert np.array_equal(p[:, 60:63], np.tile([1.0, 0.0, -1.0], (len(p), 1)).astype(np.float32))
+    assert (p[:, 58] <= 0).all() and (p[:, 59] >= 0).all()  # mHeightInside <= 0 <= mHeightOutside

@@ -1,0 +1,108 @@
+"""The BVH culling is exact-preserving: every (ray, patch) pair that passes the reference's planar gate
+(reference/bezierTriangle.cpp:124-131, computed by the oracle) must also pass the float32 slab test
+the traversal kernel runs against that patch's gate-region box (csrc/host/bvh.cpp,
+csrc/device/trace.hip `slab`).  A pair that passes the gate but misses its box would silently change
+the result; this checks it on CPU for grazing, far, random and config rays -- including the
+ill-conditioned patches whose plane passes near the origin."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from bzr_amd.configs import CONFIGS, build_lens, grid_rays
+
+
+def gate_boxes(bzr, patches):
+    L = bzr.lib()
+    fn = L.bzr_debug_gate_boxes
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
+    fn.restype = ctypes.c_int32
+    p = np.ascontiguousarray(patches, np.float32)
+    boxes = np.zeros((len(p), 6), np.float32)
+    smax = np.zeros(1, np.float32)
+    assert fn(p.ctypes.data, len(p), 264, boxes.ctypes.data, smax.ctypes.data) == 0
+    return boxes, float(smax[0])
+
+
+def slab_f32(boxes, rays):
+    """float32 replica of the kernel's slab(): hit[r, i]."""
+    f = np.float32
+    s = rays[:3].T.astype(f)[:, None, :]  # [R,1,3]
+    d = rays[3:].T.astype(f)
+    d = np.where(np.abs(d) < f(1e-20), np.copysign(f(1e-20), d), d).astype(f)
+    inv = (f(1.0) / d)[:, None, :]
+    lo, hi = boxes[None, :, :3], boxes[None, :, 3:]
+    with np.errstate(invalid="ignore", over="ignore"):
+        a = ((lo - s) * inv).astype(f)
+        b = ((hi - s) * inv).astype(f)
+    tnear = np.fmax(np.fmax(np.fmin(a[..., 0], b[..., 0]), np.fmin(a[..., 1], b[..., 1])), np.fmin(a[..., 2], b[..., 2]))
+    tfar = np.fmin(np.fmin(np.fmax(a[..., 0], b[..., 0]), np.fmax(a[..., 1], b[..., 1])), np.fmax(a[..., 2], b[..., 2]))
+    return (tnear <= tfar) & (tfar >= 0)
+
+
+def random_rays(rng, n, centre, spread, far=False):
+    c = np.asarray(centre, np.float64)
+    o = c + rng.uniform(-spread, spread, (n, 3)) * (8.0 if far else 1.5)
+    tgt = c + rng.uniform(-spread, spread, (n, 3))
+    d = tgt - o
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    # a quarter of the rays get a zeroed direction component (axis-parallel cases)
+    z = rng.random(n) < 0.25
+    d[z, rng.integers(0, 3, z.sum())] = 0.0
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    return np.concatenate([o.T, d.T]).astype(np.float32)
+
+
+def check(bzr, orc, patches, rays):
+    boxes, smax = gate_boxes(bzr, patches)
+    gate = orc.planar_gate(patches, rays)
+    near = np.abs(rays[:3]).max(axis=0) <= smax
+    hit = slab_f32(boxes, rays)
+    missed = gate & ~hit & near[:, None]
+    assert gate.sum() > 0
+    assert not missed.any(), f"{int(missed.sum())} gate-passing pairs culled, e.g. {np.argwhere(missed)[:5]}"
+    return gate.sum(), hit.sum()
+
+
+@pytest.mark.parametrize("name", ["cfg1", "cfg2", "cfg3"])
+def test_config_rays_never_culled(bzr, orc, name):
+    cfg = CONFIGS[name]
+    patches = build_lens(bzr.TriMesh, cfg.lenses[0]).bezier_patches()
+    rays = grid_rays(cfg, side=48)
+    check(bzr, orc, patches, rays)
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_random_and_grazing_rays_never_culled(bzr, orc, seed):
+    rng = np.random.default_rng(seed)
+    patches = build_lens(bzr.TriMesh, CONFIGS["cfg2"].lenses[0]).bezier_patches()
+    rays = np.concatenate([random_rays(rng, 1500, (10, 0, 0), 3.0), random_rays(rng, 500, (10, 0, 0), 3.0, far=True)], 1)
+    # refracted-ray-like origins: points on the lens surface heading inward
+    cp = patches[:, 19:22]
+    pick = rng.integers(0, len(patches), 500)
+    o = cp[pick] + rng.normal(0, 1e-3, (500, 3)).astype(np.float32)
+    d = np.array([10, 0, 0], np.float32) - o + rng.normal(0, 0.5, (500, 3)).astype(np.float32)
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    rays = np.concatenate([rays, np.concatenate([o.T, d.T]).astype(np.float32)], 1)
+    gate, hit = check(bzr, orc, patches, rays)
+    assert hit < 0.2 * rays.shape[1] * len(patches)  # and the boxes do cull
+
+
+def test_ill_conditioned_patches(bzr, orc):
+    """Lens placed so that many patch planes pass close to the origin: the gate region is far larger than
+    the flat triangle there, and the boxes must cover it."""
+    m = bzr.TriMesh().make_ellipsoid(16, 8, (1.0, 4.0, 2.0)).translate((1.3, 0.5, 0.0)).standardize()
+    patches = m.bezier_patches()
+    c = np.abs(patches[:, 3])
+    assert (c < 3e-3).sum() >= 2  # planes through (nearly) the origin
+    rng = np.random.default_rng(7)
+    rays = random_rays(rng, 3000, (1.3, 0.5, 0.0), 3.0)
+    # plus rays aimed at the ill-conditioned patches themselves
+    worst = np.argsort(c)[:8]
+    cp = patches[worst][:, 19:28].reshape(-1, 3, 3)
+    tgt = cp.mean(axis=1).repeat(125, 0) + rng.normal(0, 0.05, (1000, 3))
+    o = tgt + rng.normal(0, 2.0, (1000, 3))
+    d = tgt - o
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    rays = np.concatenate([rays, np.concatenate([o.T, d.T]).astype(np.float32)], 1)
+    check(bzr, orc, patches, rays)

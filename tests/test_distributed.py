@@ -1,0 +1,57 @@
+"""Multi-rank path on CPU (gloo, world_size 2 and 3): shard the image, trace each rank's tiles, gather to
+rank 0 and assemble -- the result must equal tracing the whole image in one process.  The per-rank
+tracer here is the oracle (CPU); on GPUs bench.py runs the same frame logic with libbzr over RCCL."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from bzr_amd import frame
+from bzr_amd.configs import CONFIGS
+
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def worker(rank, world, port, width, height, patches, result_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import pyoracle
+
+        cfg = CONFIGS["cfg2"]
+        rows, cols, rays = frame.rank_rays(cfg, rank, world, width, height)
+        o, s, g = pyoracle.trace_chain([patches], [1.3], rays, threads=2)
+        packed = torch.empty((frame.PACKED_ROWS, rays.shape[1]), dtype=torch.float32)
+        frame.pack(torch.from_numpy(o), torch.from_numpy(s.view(np.int32)), torch.from_numpy(g.view(np.int32)), packed)
+        glist = [torch.empty_like(packed) for _ in range(world)] if rank == 0 else None
+        parts = frame.gather(packed, world, rank, gather_list=glist)
+        if rank == 0:
+            r, st, sg = frame.assemble(parts, cfg, world, width, height)
+            np.savez(result_path, rays=r, status=st, seg=sg)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_frame_equals_single_process(bzr, orc, world, tmp_path):
+    cfg = CONFIGS["cfg2"]
+    patches = bzr.TriMesh().make_ellipsoid(32, 16, (1, 4, 2)).translate((10, 0, 0)).standardize().bezier_patches()
+    width, height = 128, 64 * world
+    out = tmp_path / "frame.npz"
+    mp.start_processes(worker, args=(world, free_port(), width, height, patches, str(out)), nprocs=world,
+                       join=True, start_method="spawn")
+    got = np.load(out)
+    rows, cols, rays = frame.rank_rays(cfg, 0, 1, width, height)
+    o, s, g = orc.trace_chain([patches], [1.3], rays)
+    flat = rows * width + cols
+    assert np.array_equal(got["status"][flat], s) and np.array_equal(got["seg"][flat], g)
+    assert np.array_equal(got["rays"][:, flat].view(np.uint32), o.view(np.uint32))
+    assert got["seg"].sum() > width * height  # refracted segments were traced

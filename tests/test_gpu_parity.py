@@ -229,3 +229,57 @@ def test_cfg4_full_size_properties(bzr, orc, ctx):
     wo, ws, wg = orc.trace_chain(lenses, [1.3, 1.3], sample)
     assert np.array_equal(s[torch.from_numpy(pick).cuda()].cpu().numpy().astype(np.uint32), ws)
     assert np.array_equal(o[:, torch.from_numpy(pick).cuda()].cpu().numpy().view(np.uint32), wo.view(np.uint32))
+
+
+# ---------------------------------------------------------------- culled == brute force
+def test_culled_equals_bruteforce_cfg2_full(bzr, ctx, meshes):
+    """Default (BVH-culled) chain vs the brute-force scan over the full cfg2 image: every bit equal."""
+    cfg = CONFIGS["cfg2"]
+    dm = bzr.DeviceMesh(ctx, meshes["cfg2"][0])
+    rays = grid_rays(cfg)
+    a = bzr.trace_chain(ctx, [dm], [1.3], rays)
+    b = bzr.trace_chain(ctx, [dm], [1.3], rays, mode=bzr.ACCEL_NONE)
+    for x, y in zip(a, b):
+        assert np.array_equal(x.view(np.uint32), y.view(np.uint32))
+
+
+def test_culled_equals_bruteforce_robot_and_random(bzr, orc, ctx, meshes):
+    cfg = CONFIGS["cfg3"]
+    dm = bzr.DeviceMesh(ctx, meshes["cfg3"][0])
+    rays = grid_rays(cfg, side=512)
+    a = bzr.intersect(ctx, dm, rays)
+    b = bzr.intersect(ctx, dm, rays, mode=bzr.ACCEL_NONE)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    # random rays from everywhere around the cfg2 lens, incl. axis-parallel directions and far origins
+    rng = np.random.default_rng(21)
+    n = 200000
+    o = rng.uniform(-20, 30, (n, 3)).astype(np.float32)
+    tgt = (np.array([10, 0, 0]) + rng.uniform(-2, 2, (n, 3)) * np.array([1, 4, 2])).astype(np.float32)
+    d = tgt - o
+    z = rng.random(n) < 0.2
+    d[z, rng.integers(0, 3, z.sum())] = 0.0
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    far = rng.random(n) < 0.01
+    o[far] *= 1e4  # beyond the culling radius: full-scan fallback
+    rays = np.concatenate([o.T, d.T]).astype(np.float32)
+    dm2 = bzr.DeviceMesh(ctx, meshes["cfg2"][0])
+    a = bzr.intersect(ctx, dm2, rays)
+    b = bzr.intersect(ctx, dm2, rays, mode=bzr.ACCEL_NONE)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    assert (a.view(np.uint32)[11] == 4).mean() > 0.1
+    o1, s1 = bzr.refract(ctx, dm2, 1.3, rays, None, expected_all=1)
+    o2, s2 = bzr.refract(ctx, dm2, 1.3, rays, None, expected_all=1, mode=bzr.ACCEL_NONE)
+    assert np.array_equal(s1, s2) and np.array_equal(o1.view(np.uint32), o2.view(np.uint32))
+
+
+@pytest.mark.slow
+def test_cfg5_sample_against_oracle(bzr, orc, ctx):
+    """cfg5 (301056 patches): a sample of its 8192^2 grid, culled GPU path vs the oracle."""
+    cfg = CONFIGS["cfg5"]
+    patches = build_lens(bzr.TriMesh, cfg.lenses[0]).bezier_patches()
+    r, c = pixel_coords(cfg, side=8192, order="rows")
+    pick = np.random.default_rng(5).choice(len(r), 384, replace=False)
+    rays = rays_for(cfg, r[pick], c[pick], side=8192)
+    got = bzr.intersect(ctx, bzr.DeviceMesh(ctx, patches), rays)
+    want = orc.intersect(patches, rays, threads=16)
+    assert_hits_equal(got, want, "cfg5")
