@@ -53,7 +53,7 @@ def main():
                 agg[(name, counter)].append((value, dur))
             lines.append(f"== PMC ({f.split('gpurun_out/')[-1]})")
             for (name, counter), vals in sorted(agg.items()):
-                if not name.startswith("(anonymous namespace)::k_"):
+                if "(anonymous namespace)::k_" not in name:
                     continue
                 v = sum(x for x, _ in vals) / len(vals)
                 extra = ""
