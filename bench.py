@@ -167,23 +167,27 @@ def main():
         if a.cpu_baseline == "on" and world == 1:
             base, cnt = cpu_baseline(cfg, side, patches, ris, a.cpu_sample_stride)
         if cnt and cnt["segments"]:
-            newton_per_seg = (cnt["newton"] + cnt["follow"]) / cnt["segments"]
+            newton_per_seg = cnt["newton"] / cnt["segments"]
+            follow_per_seg = cnt["follow"] / cnt["segments"]
             tests_per_seg = cnt["tests"] / cnt["segments"]
         else:  # SURVEY.md 8d measured values for cfg2
-            newton_per_seg, tests_per_seg = 1.51, float(n_patch) / len(patches)
+            newton_per_seg, follow_per_seg, tests_per_seg = 1.258, 0.057, float(n_patch) / len(patches)
         # algorithmic work per step on rank 0: F_seg = 33 N_b + 1750 (N_cand + N_follow)
         seg_r0 = seg_local
-        planar_flops = seg_r0 * FLOPS_PLANAR * tests_per_seg
-        newton_flops = seg_r0 * (FLOPS_NEWTON * newton_per_seg + FLOPS_REFRACT)
+        work = {
+            "k_traverse": (seg_r0 * FLOPS_PLANAR * tests_per_seg,
+                           "brute-force-equivalent planar tests 33 N_b per segment (culling skips most of them)"),
+            "k_newton": (seg_r0 * FLOPS_NEWTON * newton_per_seg, "Newton stage 1750 flops per candidate pair"),
+            "k_follow": (seg_r0 * FLOPS_NEWTON * follow_per_seg, "Newton stage 1750 flops per follow-side retry"),
+            "k_finish": (seg_r0 * FLOPS_REFRACT, "Snell step 30 flops per segment"),
+        }
+        all_flops = sum(f for f, _ in work.values())
         per_kernel = {}
         for name, (ms, calls) in kernels.items():
             per_step = ms / a.steps
-            if name in ("k_resolve_refract", "k_resolve_hits"):
-                fl, what = newton_flops, "Newton stage + refraction of every segment (oracle-measured candidate rate)"
-            elif name == "k_traverse":
-                fl, what = planar_flops, "brute-force-equivalent planar tests (SURVEY 8d: may exceed 1 when culled)"
-            else:
-                fl, what = planar_flops + newton_flops, "brute-force segment work F_seg"
+            fl, what = work.get(name, (all_flops, "brute-force segment work F_seg"))
+            if name in ("bucket", "k_overflow"):
+                fl, what = 0.0, "bookkeeping (prefix sum + scatter) / overflow rays' full scan"
             per_kernel[name] = {"ms_per_step": round(per_step, 4), "launches_per_step": calls / a.steps,
                                 "avg_launch_ms": round(ms / calls, 4),
                                 "alg_tflops": round(fl / (per_step * 1e-3) / 1e12, 3), "work": what}
@@ -232,7 +236,8 @@ def main():
                 "hbm_alg_bytes_per_step": alg_bytes,
                 "hbm_achieved_GBps": round(alg_bytes / (chain_ms * 1e-3) / 1e9, 3),
                 "hbm_frac": round(alg_bytes / (chain_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 6),
-                "work_per_segment": {"planar_tests": round(tests_per_seg, 2), "newton": round(newton_per_seg, 4)},
+                "work_per_segment": {"planar_tests": round(tests_per_seg, 2), "newton": round(newton_per_seg, 4),
+                                     "follow": round(follow_per_seg, 4)},
             },
             "cpu_baseline": base,
         }

@@ -67,7 +67,10 @@ struct Patch {  // registers holding one record
   f3 da, db;
 };
 
-__device__ __forceinline__ Patch load_patch(const float *__restrict__ r) {
+// Per-lane record: r is a generic pointer.  Wave-uniform record: r is a constant-address-space
+// pointer (load_patch_uniform), which the backend fetches with scalar loads into SGPRs.
+template <typename Ptr>
+__device__ __forceinline__ Patch load_patch(Ptr r) {
   Patch p;
   p.n = mk(r[0], r[1], r[2]);
   p.c = r[3];
@@ -85,6 +88,11 @@ __device__ __forceinline__ Patch load_patch(const float *__restrict__ r) {
   p.da = mk(r[rec::kDirA], r[rec::kDirA + 1], r[rec::kDirA + 2]);
   p.db = mk(r[rec::kDirB], r[rec::kDirB + 1], r[rec::kDirB + 2]);
   return p;
+}
+
+typedef __attribute__((address_space(4))) const float const_float;
+__device__ __forceinline__ Patch load_patch_uniform(const float *base, uint32_t index) {
+  return load_patch((const const_float *)(uintptr_t)(base + (size_t)rec::kWords * index));
 }
 
 __device__ __forceinline__ f3 matvec(const float *m, f3 v) {  // Eigen row redux over a col-major matrix

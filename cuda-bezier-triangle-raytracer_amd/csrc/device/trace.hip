@@ -19,6 +19,9 @@
 //   brute force       (BZR_ACCEL_NONE) the reference's own scan: every patch's 64-byte planar
 //                     record fetched once per wave with scalar loads, Newton for passing lanes.
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
 
 #include <cstdio>
 #include <cstring>
@@ -186,36 +189,6 @@ __device__ __forceinline__ Hit mesh_intersect_scan(const MeshView &m, f3 s, f3 d
   return best;
 }
 
-// BezierMesh::intersect from a candidate list.  The reference keeps the first (lowest index)
-// candidate with the smallest t; over an unordered list that is the (t, index) lexicographic
-// minimum among t < FLT_MAX.  count > kMaxCand: the full in-order scan.
-__device__ __forceinline__ Hit mesh_intersect_list(const MeshView &m, f3 s, f3 d, const uint32_t *__restrict__ cand,
-                                                   uint32_t count, uint32_t n, uint32_t i, uint32_t &patch) {
-  Hit best = no_hit();
-  patch = 0xFFFFFFFFu;
-  uint32_t best_b = 0xFFFFFFFFu;
-  bool scan = count > kMaxCand;
-  uint32_t trips = scan ? m.n : count;
-  for (uint32_t j = 0; j < trips; ++j) {
-    uint32_t b;
-    if (scan) {
-      b = j;
-      const float4 *q = m.planar + 4u * b;
-      if (!planar_gate(q[0], q[1], q[2], q[3], s, d)) continue;
-    } else {
-      b = cand[(size_t)j * n + i];
-    }
-    uint32_t src;
-    Hit h = evaluate_patch(m, b, s, d, src);
-    if (h.what == kIntersect && (h.t < best.t || (h.t == best.t && best_b != 0xFFFFFFFFu && b < best_b))) {
-      best = h;
-      patch = src;
-      best_b = b;
-    }
-  }
-  return best;
-}
-
 // The refraction of BezierLens::refract after the mesh intersection.  Returns the status;
 // o_s/o_d = refracted ray when status != NONE.
 __device__ __forceinline__ uint32_t refract_hit(const Hit &h, float ri, f3 s, f3 d, uint32_t expected, f3 &o_s,
@@ -271,18 +244,111 @@ __device__ __forceinline__ bool slab(float4 lo, float4 hi, f3 s, f3 inv) {
   return tnear <= tfar && tfar >= 0.0f;
 }
 
-// Candidate search for one BezierMesh::intersect per active lane.  `alive` (optional): a ray is
-// traced iff alive[i] != BZR_RR_NONE.  Writes count[i] (kOverflow = resolve by full scan) and up
-// to kMaxCand patch indices cand[j*n + i].
-__global__ __launch_bounds__(kBlock) void k_traverse(MeshView m, const float *__restrict__ rays,
-                                                     const uint32_t *__restrict__ alive, uint32_t n,
-                                                     uint32_t *__restrict__ cand, uint32_t *__restrict__ count) {
+// Per-segment pipeline of the culled path (one BezierMesh::intersect per ray of a chunk of n rays;
+// external arrays -- rays, alive, outputs -- are indexed off + i with row stride ld):
+//   k_traverse  BVH walk, exact planar gate -> up to kMaxCand candidates per ray, a per-patch
+//               histogram (rank of each (ray, patch) pair within its patch bucket) and the list
+//               of rays that need the full scan (list/stack overflow, origin beyond s_max)
+//   scan        exclusive sum of the histogram (hipCUB) -> bucket offsets, total pair count
+//   k_scatter   (ray, patch) pairs into patch-major order
+//   k_newton    the Newton stage per pair; a wave holds <= a few distinct patches, processed one at a
+//               time with the patch record in scalar registers (uniform loads); hits go to a per-pair
+//               slot and a per-ray 64-bit atomicMin on (t order key, pair index)
+//   k_follow    follow-side results: the named neighbour with cNone, per lane
+//   k_finish    winner -> BezierIntersection / refraction, for rays not on the overflow list
+//   k_overflow  the reference's in-order scan for the overflow list
+// Pair indices are patch-major, so for one ray (t, pair index) orders like (t, scanned patch
+// index): the atomicMin winner is the reference's strict-< in-order winner.
+struct Work {
+  uint32_t *hist;    // [nb + 1] pair counts per patch (hist[nb] = 0), then ctr[4]
+  uint32_t *ctr;     // [0] follow count, [1] overflow count
+  uint32_t *offs;    // [nb + 1] exclusive prefix of hist; offs[nb] = pair count
+  uint32_t *cand;    // [kMaxCand][n]
+  uint32_t *rank;    // [kMaxCand][n]
+  uint32_t *count;   // [n]
+  unsigned long long *key;  // [n]
+  float *slot;       // [kSlotWords][cap] per-pair hit
+  uint2 *pairs;      // [cap] (ray, patch)
+  uint32_t *fol;     // [cap] pair | what << 30
+  uint32_t *ovf;     // [n]
+  void *cub;
+  size_t cub_bytes;
+  uint32_t cap;      // kMaxCand * chunk
+};
+constexpr uint32_t kSlotWords = 12;  // t, point, cos, bary, normal, source patch
+
+enum OutMode { kModeHits = 0, kModeRefract = 1, kModeStage = 2 };
+struct Out {
+  float *hits;               // kModeHits: SoA [13][ld]
+  float *rays;               // kModeRefract: output rays; kModeStage: rays in flight (in place)
+  const uint32_t *expected;  // per ray, or null -> expected_all
+  uint32_t expected_all;
+  uint32_t *status;
+  uint32_t *segments;        // kModeStage, optional
+  float ri;
+};
+
+template <int kMode>
+__device__ __forceinline__ void emit(const Out &o, uint32_t ld, uint32_t gi, f3 s, f3 d, const Hit &h, uint32_t patch) {
+  if (kMode == kModeHits) {
+    store_hit(o.hits, ld, gi, h, patch);
+  } else {
+    f3 os, od;
+    uint32_t st = refract_hit(h, o.ri, s, d, o.expected ? o.expected[gi] : o.expected_all, os, od);
+    if (kMode == kModeRefract || st != BZR_RR_NONE) {
+      if (st == BZR_RR_NONE) {
+        os = s;
+        od = d;
+      }
+      store_ray(o.rays, ld, gi, os, od);
+    }
+    o.status[gi] = st;
+    if (kMode == kModeStage && o.segments) o.segments[gi] += 1u;
+  }
+}
+
+// Monotone map of t to uint32 (IEEE total order; -0 canonicalised to +0 so they tie like `<`).
+__device__ __forceinline__ uint32_t t_order(float t) {
+  uint32_t u = __float_as_uint(t == 0.0f ? 0.0f : t);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+// Number of lanes below this one in `mask`.
+__device__ __forceinline__ uint32_t lanes_below(unsigned long long mask) {
+  return __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(mask >> 32),
+                                   __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(mask), 0u));
+}
+
+// One intersecting pair result: its slot, then the ray's running (t, pair) minimum.  t that cannot
+// beat the reference's initial FLT_MAX (NaN, FLT_MAX, +inf) is dropped; -0 ties with +0.
+__device__ __forceinline__ void record(float *__restrict__ slot, uint32_t cap, uint32_t p, const Hit &h, uint32_t src,
+                                       unsigned long long *key) {
+  if (!(h.t < FLT_MAX)) return;
+  slot[p] = h.t;
+  slot[(size_t)1 * cap + p] = h.point.x;
+  slot[(size_t)2 * cap + p] = h.point.y;
+  slot[(size_t)3 * cap + p] = h.point.z;
+  slot[(size_t)4 * cap + p] = h.cs;
+  slot[(size_t)5 * cap + p] = h.bary.x;
+  slot[(size_t)6 * cap + p] = h.bary.y;
+  slot[(size_t)7 * cap + p] = h.bary.z;
+  slot[(size_t)8 * cap + p] = h.normal.x;
+  slot[(size_t)9 * cap + p] = h.normal.y;
+  slot[(size_t)10 * cap + p] = h.normal.z;
+  slot[(size_t)11 * cap + p] = __uint_as_float(src);
+  atomicMin(key, ((unsigned long long)t_order(h.t) << 32) | p);
+}
+
+// Candidate search.  `alive` (optional): a ray is traced iff alive[off + i] != BZR_RR_NONE.
+__global__ __launch_bounds__(kBlock) void k_traverse(MeshView m, const float *__restrict__ rays, uint32_t ld,
+                                                     uint32_t off, const uint32_t *__restrict__ alive, uint32_t n,
+                                                     Work w) {
   __shared__ uint32_t stack[kWaves][kStack];
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  const uint32_t w = threadIdx.x >> 6;
-  bool active = i < n && (alive == nullptr || alive[i] != BZR_RR_NONE);
+  const uint32_t wv = threadIdx.x >> 6;
+  bool active = i < n && (alive == nullptr || alive[off + i] != BZR_RR_NONE);
   f3 s = mk(0.0f, 0.0f, 0.0f), d = s;
-  if (i < n) load_ray(rays, n, i, s, d);
+  if (i < n) load_ray(rays, ld, off + i, s, d);
   uint32_t cnt = 0;
   // gate-region boxes hold for ray origins within s_max (bvh.cpp); farther rays take the full scan
   if (active && !(fmaxf(fmaxf(fabsf(s.x), fabsf(s.y)), fabsf(s.z)) <= m.s_max)) {
@@ -292,11 +358,11 @@ __global__ __launch_bounds__(kBlock) void k_traverse(MeshView m, const float *__
   f3 inv = mk(safe_inv(d.x), safe_inv(d.y), safe_inv(d.z));
   int sp = 0;
   if (m.n > 0 && __any(active)) {
-    stack[w][0] = 0u;
+    stack[wv][0] = 0u;
     sp = 1;
   }
   while (sp > 0) {
-    uint32_t node = __builtin_amdgcn_readfirstlane(stack[w][--sp]);
+    uint32_t node = __builtin_amdgcn_readfirstlane(stack[wv][--sp]);
     const bzr_host::BvhNode nd = m.nodes[node];
     bool hit = active && slab(make_float4(nd.lo[0], nd.lo[1], nd.lo[2], 0.0f),
                               make_float4(nd.hi[0], nd.hi[1], nd.hi[2], 0.0f), s, inv);
@@ -309,61 +375,176 @@ __global__ __launch_bounds__(kBlock) void k_traverse(MeshView m, const float *__
         uint32_t b = m.order[k];
         const float4 *q = m.planar + 4u * b;
         if (h2 && planar_gate(q[0], q[1], q[2], q[3], s, d)) {
-          if (cnt < kMaxCand) cand[(size_t)cnt * n + i] = b;
+          if (cnt < kMaxCand) w.cand[(size_t)cnt * n + i] = b;
           cnt = cnt < kMaxCand ? cnt + 1 : kOverflow;
         }
       }
     } else if (sp + 2 <= kStack) {
-      stack[w][sp] = nd.b;
-      stack[w][sp + 1] = nd.a;
+      stack[wv][sp] = nd.b;
+      stack[wv][sp + 1] = nd.a;
       sp += 2;
     } else {  // traversal stack exhausted: resolve these rays with the full scan
       if (hit) cnt = kOverflow;
     }
   }
-  if (i < n) count[i] = cnt;
-}
-
-__global__ __launch_bounds__(kBlock) void k_resolve_hits(MeshView m, const float *__restrict__ rays,
-                                                         const uint32_t *__restrict__ cand,
-                                                         const uint32_t *__restrict__ count, uint32_t n,
-                                                         float *__restrict__ hits) {
-  uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
-  f3 s, d;
-  load_ray(rays, n, i, s, d);
-  uint32_t patch;
-  Hit h = mesh_intersect_list(m, s, d, cand, count[i], n, i, patch);
-  store_hit(hits, n, i, h, patch);
-}
-
-// One refract() per ray.  kStage == false (bzr_refract): every ray, expected from the arrays,
-// output = refracted ray or the input ray.  kStage == true (one step of the chain): only rays with
-// status[i] != NONE, rays/status updated in place, segments[i] += 1.
-template <bool kStage>
-__global__ __launch_bounds__(kBlock) void k_resolve_refract(MeshView m, const float *rays_in,
-                                                            const uint32_t *__restrict__ expected,
-                                                            uint32_t expected_all, const uint32_t *__restrict__ cand,
-                                                            const uint32_t *__restrict__ count, uint32_t n,
-                                                            float *rays_out, uint32_t *__restrict__ status,
-                                                            uint32_t *__restrict__ segments) {
-  uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  if (i >= n) return;
-  if (kStage && status[i] == BZR_RR_NONE) return;
-  f3 s, d, os, od;
-  load_ray(rays_in, n, i, s, d);
-  uint32_t patch;
-  Hit h = mesh_intersect_list(m, s, d, cand, count[i], n, i, patch);
-  uint32_t st = refract_hit(h, m.ri, s, d, expected ? expected[i] : expected_all, os, od);
-  if (st != BZR_RR_NONE || !kStage) {
-    if (st == BZR_RR_NONE) {
-      os = s;
-      od = d;
+  w.count[i] = cnt;
+  w.key[i] = ~0ull;
+  if (cnt > kMaxCand) w.ovf[atomicAdd(&w.ctr[1], 1u)] = i;
+  // Rank of each (ray, patch) pair within its patch bucket.  Neighbouring rays mostly share
+  // patches, so the lanes of a wave that name the same patch take one atomicAdd together.
+  const uint32_t listed = cnt <= kMaxCand ? cnt : 0u;
+  for (uint32_t j = 0; __any(j < listed); ++j) {
+    bool pend = j < listed;
+    const uint32_t b = pend ? w.cand[(size_t)j * n + i] : 0u;
+    for (;;) {
+      const unsigned long long mask = __ballot(pend);
+      if (mask == 0ull) break;
+      const uint32_t b0 = __builtin_amdgcn_readlane(b, __builtin_ctzll(mask));
+      const bool same = pend && b == b0;
+      const unsigned long long group = __ballot(same);
+      const uint32_t leader = __builtin_ctzll(group);
+      uint32_t base = 0;
+      if ((threadIdx.x & 63u) == leader) base = atomicAdd(&w.hist[b0], (uint32_t)__popcll(group));
+      base = __builtin_amdgcn_readlane(base, leader);
+      if (same) {
+        w.rank[(size_t)j * n + i] = base + lanes_below(group);
+        pend = false;
+      }
     }
-    store_ray(rays_out, n, i, os, od);
   }
-  status[i] = st;
-  if (kStage && segments) segments[i] += 1u;
+}
+
+__global__ __launch_bounds__(kBlock) void k_scatter(uint32_t n, Work w) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  uint32_t c = w.count[i];
+  if (c > kMaxCand) return;
+  for (uint32_t j = 0; j < c; ++j) {
+    uint32_t b = w.cand[(size_t)j * n + i];
+    w.pairs[w.offs[b] + w.rank[(size_t)j * n + i]] = make_uint2(i, b);
+  }
+}
+
+// `full` is a separate __restrict__ argument (noalias: the kernel's stores cannot clobber it), so the
+// wave-uniform patch record below is fetched with scalar loads into SGPRs.
+__global__ __launch_bounds__(kBlock) void k_newton(const float *__restrict__ full, const float *__restrict__ rays,
+                                                   uint32_t ld, uint32_t off, const uint32_t *__restrict__ total,
+                                                   const uint2 *__restrict__ pairs, float *__restrict__ slot,
+                                                   uint32_t cap, unsigned long long *__restrict__ key,
+                                                   uint32_t *__restrict__ fol, uint32_t *__restrict__ nfol) {
+  const uint32_t P = __builtin_amdgcn_readfirstlane(*total);
+  for (uint32_t base = blockIdx.x * kBlock; base < P; base += gridDim.x * kBlock) {
+    const uint32_t p = base + threadIdx.x;
+    bool todo = p < P;
+    uint2 pr = todo ? pairs[p] : make_uint2(0u, 0u);
+    f3 s = mk(0.0f, 0.0f, 0.0f), d = s;
+    if (todo) load_ray(rays, ld, off + pr.x, s, d);
+    for (;;) {
+      unsigned long long mask = __ballot(todo);
+      if (mask == 0ull) break;
+      // the next patch of this wave, wave-uniform: its record is fetched with scalar loads
+      const uint32_t b0 = __builtin_amdgcn_readlane(pr.y, __builtin_ctzll(mask));
+      // fetched before the branch: inside it the compiler would substitute the per-lane pr.y for b0
+      const Patch pa = load_patch_uniform(full, b0);
+      if (todo && pr.y == b0) {
+        todo = false;
+        Hit h = patch_intersect(pa, s, d, false);
+        if (h.what <= kFollow2)
+          fol[atomicAdd(nfol, 1u)] = p | (h.what << 30);
+        else if (h.what == kIntersect)
+          record(slot, cap, p, h, b0, &key[pr.x]);
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_follow(MeshView m, const float *__restrict__ rays, uint32_t ld,
+                                                   uint32_t off, Work w) {
+  const uint32_t F = __builtin_amdgcn_readfirstlane(w.ctr[0]);
+  for (uint32_t q = blockIdx.x * kBlock + threadIdx.x; q < F; q += gridDim.x * kBlock) {
+    const uint32_t e = w.fol[q], p = e & 0x3FFFFFFFu, what = e >> 30;
+    const uint2 pr = w.pairs[p];
+    f3 s, d;
+    load_ray(rays, ld, off + pr.x, s, d);
+    const uint32_t nbr = __float_as_uint(m.full[(size_t)rec::kWords * pr.y + rec::kNeigh + what]);
+    Patch pa = load_patch(m.full + (size_t)rec::kWords * nbr);
+    Hit h = patch_intersect(pa, s, d, true);
+    if (h.what == kIntersect) record(w.slot, w.cap, p, h, nbr, &w.key[pr.x]);
+  }
+}
+
+template <int kMode>
+__global__ __launch_bounds__(kBlock) void k_finish(const float *rays, uint32_t ld, uint32_t off, uint32_t n, Work w,
+                                                   Out o) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t gi = off + i;
+  if (kMode == kModeStage && o.status[gi] == BZR_RR_NONE) return;
+  if (w.count[i] > kMaxCand) return;  // k_overflow
+  f3 s, d;
+  load_ray(rays, ld, gi, s, d);
+  Hit h = no_hit();
+  uint32_t patch = 0xFFFFFFFFu;
+  const unsigned long long k = w.key[i];
+  if (k != ~0ull) {
+    const uint32_t p = static_cast<uint32_t>(k);
+    const size_t c = w.cap;
+    h.t = w.slot[p];
+    h.point = mk(w.slot[c + p], w.slot[2 * c + p], w.slot[3 * c + p]);
+    h.cs = w.slot[4 * c + p];
+    h.bary = mk(w.slot[5 * c + p], w.slot[6 * c + p], w.slot[7 * c + p]);
+    h.normal = mk(w.slot[8 * c + p], w.slot[9 * c + p], w.slot[10 * c + p]);
+    h.what = kIntersect;
+    patch = __float_as_uint(w.slot[11 * c + p]);
+  }
+  emit<kMode>(o, ld, gi, s, d, h, patch);
+}
+
+// The rays k_traverse could not take, one wave per ray: lane l scans patches l, l+64, ... in index
+// order (strict <, so per lane the lowest index wins ties), then the wave takes the (t, index)
+// lexicographic minimum -- the winner of the reference's single in-order scan.
+__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v) {
+#pragma unroll
+  for (int k = 32; k >= 1; k >>= 1) {
+    unsigned long long o = __shfl_xor(v, k, 64);
+    v = o < v ? o : v;
+  }
+  return v;
+}
+
+template <int kMode>
+__global__ __launch_bounds__(kBlock) void k_overflow(MeshView m, const float *rays, uint32_t ld, uint32_t off, Work w,
+                                                     Out o) {
+  const uint32_t V = __builtin_amdgcn_readfirstlane(w.ctr[1]);
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t nwaves = gridDim.x * kWaves;
+  for (uint32_t q = blockIdx.x * kWaves + (threadIdx.x >> 6); q < V; q += nwaves) {
+    const uint32_t gi = off + w.ovf[q];
+    f3 s, d;
+    load_ray(rays, ld, gi, s, d);
+    Hit best = no_hit();
+    uint32_t best_b = 0xFFFFFFFFu, best_src = 0xFFFFFFFFu;
+    for (uint32_t b = lane; b < m.n; b += 64u) {
+      const float4 *qq = m.planar + 4u * b;
+      if (!planar_gate(qq[0], qq[1], qq[2], qq[3], s, d)) continue;
+      uint32_t src;
+      Hit h = evaluate_patch(m, b, s, d, src);
+      if (h.what == kIntersect && h.t < best.t) {
+        best = h;
+        best_b = b;
+        best_src = src;
+      }
+    }
+    const unsigned long long mine =
+        best_b != 0xFFFFFFFFu ? ((unsigned long long)t_order(best.t) << 32) | best_b : ~0ull;
+    const unsigned long long win = wave_min_u64(mine);
+    if (win == ~0ull) {
+      if (lane == 0) emit<kMode>(o, ld, gi, s, d, no_hit(), 0xFFFFFFFFu);
+    } else if (mine == win) {
+      emit<kMode>(o, ld, gi, s, d, best, best_src);
+    }
+  }
 }
 
 __global__ void k_fill(uint32_t *__restrict__ a, uint32_t value, uint32_t n) {
@@ -496,17 +677,6 @@ bzr_status check_ctx_mesh(bzr_ctx *ctx, const bzr_mesh *mesh) {
   return BZR_OK;
 }
 
-// candidate lists for n rays: kMaxCand * n + n words of the context's work area
-bzr_status work_lists(bzr_ctx *ctx, uint32_t n, uint32_t *&cand, uint32_t *&count) {
-  if (bzr_status s = ensure_buffer(ctx->work, ctx->work_bytes,
-                                   round256((size_t)kMaxCand * n * 4) + round256((size_t)n * 4)))
-    return s;
-  Staging st{static_cast<char *>(ctx->work)};
-  cand = st.take<uint32_t>((size_t)kMaxCand * n);
-  count = st.take<uint32_t>(n);
-  return BZR_OK;
-}
-
 bool use_scan(uint32_t flags) { return (flags & BZR_ACCEL_NONE) != 0; }
 
 hipEvent_t take_event(bzr_ctx *ctx) {
@@ -523,17 +693,93 @@ hipEvent_t take_event(bzr_ctx *ctx) {
 // Launch on the context's stream; with timing enabled, bracket the launch with events.
 template <typename... Args>
 void launch(bzr_ctx *ctx, int kernel_id, void (*kernel)(Args...), dim3 grid, typename std::decay<Args>::type... args) {
+  const bool timed = ctx->timing && kernel_id >= 0;
   hipEvent_t a = nullptr, b = nullptr;
-  if (ctx->timing) {
+  if (timed) {
     a = take_event(ctx);
     b = take_event(ctx);
     (void)hipEventRecord(a, ctx->stream);
   }
   hipLaunchKernelGGL(kernel, grid, dim3(kBlock), 0, ctx->stream, args...);
-  if (ctx->timing) {
+  if (timed) {
     (void)hipEventRecord(b, ctx->stream);
     ctx->marks.push_back({kernel_id, a, b});
   }
+}
+
+// Event bracket around a group of launches (timing enabled only).
+struct Span {
+  bzr_ctx *ctx;
+  int id;
+  hipEvent_t a = nullptr;
+  Span(bzr_ctx *c, int kernel_id) : ctx(c), id(kernel_id) {
+    if (ctx->timing) {
+      a = take_event(ctx);
+      (void)hipEventRecord(a, ctx->stream);
+    }
+  }
+  ~Span() {
+    if (!a) return;
+    hipEvent_t b = take_event(ctx);
+    (void)hipEventRecord(b, ctx->stream);
+    ctx->marks.push_back({id, a, b});
+  }
+};
+
+// Workspace of the culled path for chunks of up to `chunk` rays over meshes of up to `nb` patches.
+bzr_status ensure_work(bzr_ctx *ctx, uint32_t chunk, uint32_t nb, Work &w) {
+  size_t cub_bytes = 0;
+  BZR_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, cub_bytes, static_cast<uint32_t *>(nullptr),
+                                           static_cast<uint32_t *>(nullptr), nb + 1, ctx->stream));
+  const size_t cap = (size_t)kMaxCand * chunk;
+  const size_t bytes = round256((size_t)(nb + 5) * 4) + round256((size_t)(nb + 1) * 4) + 2 * round256(cap * 4) +
+                       round256((size_t)chunk * 4) + round256((size_t)chunk * 8) + round256(kSlotWords * cap * 4) +
+                       round256(cap * 8) + round256(cap * 4) + round256((size_t)chunk * 4) + round256(cub_bytes);
+  if (bzr_status s = ensure_buffer(ctx->work, ctx->work_bytes, bytes)) return s;
+  Staging st{static_cast<char *>(ctx->work)};
+  w.hist = st.take<uint32_t>(nb + 5);
+  w.ctr = w.hist + nb + 1;
+  w.offs = st.take<uint32_t>(nb + 1);
+  w.cand = st.take<uint32_t>(cap);
+  w.rank = st.take<uint32_t>(cap);
+  w.count = st.take<uint32_t>(chunk);
+  w.key = st.take<unsigned long long>(chunk);
+  w.slot = st.take<float>(kSlotWords * cap);
+  w.pairs = st.take<uint2>(cap);
+  w.fol = st.take<uint32_t>(cap);
+  w.ovf = st.take<uint32_t>(chunk);
+  w.cub = st.take<char>(cub_bytes ? cub_bytes : 1);
+  w.cub_bytes = cub_bytes;
+  w.cap = static_cast<uint32_t>(cap);
+  return BZR_OK;
+}
+
+// Chunk size of the culled path: bounds the workspace (~560 B per ray) for very large batches.
+constexpr uint32_t kChunk = 1u << 22;
+uint32_t chunk_for(uint32_t n) { return n < kChunk ? n : kChunk; }
+
+// One BezierMesh::intersect per ray of rays [off, off + n) (+ refraction, per kMode).
+template <int kMode>
+bzr_status run_culled(bzr_ctx *ctx, const MeshView &mv, const float *rays, uint32_t ld, uint32_t off, uint32_t n,
+                      const uint32_t *alive, const Out &o, Work &w) {
+  const uint32_t nb = mv.n;
+  BZR_HIP(hipMemsetAsync(w.hist, 0, (size_t)(nb + 5) * 4, ctx->stream));
+  launch(ctx, BZR_KERNEL_TRAVERSE, k_traverse, dim3(grid_for(n)), mv, rays, ld, off, alive, n, w);
+  {
+    Span sp(ctx, BZR_KERNEL_BUCKET);
+    BZR_HIP(hipcub::DeviceScan::ExclusiveSum(w.cub, w.cub_bytes, w.hist, w.offs, nb + 1, ctx->stream));
+    launch(ctx, -1, k_scatter, dim3(grid_for(n)), n, w);
+  }
+  const uint32_t gn = std::min<uint32_t>(std::max<uint32_t>(grid_for(2 * n), 1u), 16384u);
+  launch(ctx, BZR_KERNEL_NEWTON, k_newton, dim3(gn), mv.full, rays, ld, off, w.offs + nb, w.pairs, w.slot, w.cap, w.key,
+         w.fol, w.ctr);
+  launch(ctx, BZR_KERNEL_FOLLOW, k_follow, dim3(std::min<uint32_t>(grid_for(n / 8 + 1), 1024u)), mv, rays, ld, off,
+         w);
+  launch(ctx, BZR_KERNEL_FINISH, k_finish<kMode>, dim3(grid_for(n)), rays, ld, off, n, w, o);
+  launch(ctx, BZR_KERNEL_OVERFLOW, k_overflow<kMode>, dim3(std::min<uint32_t>((n + kWaves - 1) / kWaves, 2048u)), mv,
+         rays, ld, off, w, o);
+  BZR_HIP(hipGetLastError());
+  return BZR_OK;
 }
 
 }  // namespace
@@ -739,12 +985,14 @@ extern "C" bzr_status bzr_intersect(bzr_ctx *ctx, const bzr_mesh *mesh, const fl
   if (use_scan(flags)) {
     launch(ctx, BZR_KERNEL_INTERSECT_SCAN, k_intersect_scan, dim3(grid_for(n)), mv, d_rays, n, d_hits);
   } else {
-    uint32_t *cand, *count;
-    if (bzr_status s = work_lists(ctx, n, cand, count)) return s;
-    launch(ctx, BZR_KERNEL_TRAVERSE, k_traverse, dim3(grid_for(n)), mv, d_rays,
-                       static_cast<const uint32_t *>(nullptr), n, cand, count);
-    launch(ctx, BZR_KERNEL_RESOLVE_HITS, k_resolve_hits, dim3(grid_for(n)), mv, d_rays, cand, count, n,
-                       d_hits);
+    Work w;
+    const uint32_t ch = chunk_for(n);
+    if (bzr_status s = ensure_work(ctx, ch, mesh->n, w)) return s;
+    Out o{};
+    o.hits = d_hits;
+    for (uint32_t off = 0; off < n; off += ch)
+      if (bzr_status s = run_culled<kModeHits>(ctx, mv, d_rays, n, off, std::min(ch, n - off), nullptr, o, w))
+        return s;
   }
   BZR_HIP(hipGetLastError());
   if (host) {
@@ -819,12 +1067,18 @@ extern "C" bzr_status bzr_refract(bzr_ctx *ctx, const bzr_mesh *mesh, float ri, 
     launch(ctx, BZR_KERNEL_REFRACT_SCAN, k_refract_scan, dim3(grid_for(n)), mv, d_rays, d_exp, expected_all,
                        n, d_out, d_st);
   } else {
-    uint32_t *cand, *count;
-    if (bzr_status s = work_lists(ctx, n, cand, count)) return s;
-    launch(ctx, BZR_KERNEL_TRAVERSE, k_traverse, dim3(grid_for(n)), mv, d_rays,
-                       static_cast<const uint32_t *>(nullptr), n, cand, count);
-    launch(ctx, BZR_KERNEL_RESOLVE_REFRACT, k_resolve_refract<false>, dim3(grid_for(n)), mv, d_rays, d_exp,
-                       expected_all, cand, count, n, d_out, d_st, static_cast<uint32_t *>(nullptr));
+    Work w;
+    const uint32_t ch = chunk_for(n);
+    if (bzr_status s = ensure_work(ctx, ch, mesh->n, w)) return s;
+    Out o{};
+    o.rays = d_out;
+    o.expected = d_exp;
+    o.expected_all = expected_all;
+    o.status = d_st;
+    o.ri = ri;
+    for (uint32_t off = 0; off < n; off += ch)
+      if (bzr_status s = run_culled<kModeRefract>(ctx, mv, d_rays, n, off, std::min(ch, n - off), nullptr, o, w))
+        return s;
   }
   BZR_HIP(hipGetLastError());
   if (host) {
@@ -871,19 +1125,26 @@ extern "C" bzr_status bzr_trace_chain(bzr_ctx *ctx, const bzr_mesh *const *lense
     BZR_HIP(hipGetLastError());
   } else {
     // stage by stage: out_rays holds the rays in flight, out_status != NONE marks them alive
-    uint32_t *cand, *count;
-    if (bzr_status s = work_lists(ctx, n, cand, count)) return s;
+    uint32_t nb = 0;
+    for (uint32_t l = 0; l < nlens; ++l) nb = std::max(nb, set.lens[l].n);
+    Work w;
+    const uint32_t ch = chunk_for(n);
+    if (bzr_status s = ensure_work(ctx, ch, nb, w)) return s;
     BZR_HIP(hipMemcpyAsync(d_out, d_rays, (size_t)n * 24, hipMemcpyDeviceToDevice, ctx->stream));
     hipLaunchKernelGGL(k_fill, dim3(grid_for(n)), dim3(kBlock), 0, ctx->stream, d_st, uint32_t(BZR_RR_INSIDE), n);
     if (d_seg) hipLaunchKernelGGL(k_fill, dim3(grid_for(n)), dim3(kBlock), 0, ctx->stream, d_seg, 0u, n);
-    for (uint32_t l = 0; l < nlens; ++l) {
-      for (uint32_t j = 0; j < 2; ++j) {
-        launch(ctx, BZR_KERNEL_TRAVERSE, k_traverse, dim3(grid_for(n)), set.lens[l], d_out, d_st, n,
-                           cand, count);
-        launch(ctx, BZR_KERNEL_RESOLVE_REFRACT, k_resolve_refract<true>, dim3(grid_for(n)), set.lens[l], d_out,
-                           static_cast<const uint32_t *>(nullptr),
-                           j == 0 ? uint32_t(BZR_RR_INSIDE) : uint32_t(BZR_RR_OUTSIDE), cand, count, n, d_out, d_st,
-                           d_seg);
+    for (uint32_t off = 0; off < n; off += ch) {
+      const uint32_t m = std::min(ch, n - off);
+      for (uint32_t l = 0; l < nlens; ++l) {
+        for (uint32_t j = 0; j < 2; ++j) {
+          Out o{};
+          o.rays = d_out;
+          o.expected_all = j == 0 ? uint32_t(BZR_RR_INSIDE) : uint32_t(BZR_RR_OUTSIDE);
+          o.status = d_st;
+          o.segments = d_seg;
+          o.ri = set.lens[l].ri;
+          if (bzr_status s = run_culled<kModeStage>(ctx, set.lens[l], d_out, n, off, m, d_st, o, w)) return s;
+        }
       }
     }
     BZR_HIP(hipGetLastError());

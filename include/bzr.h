@@ -105,14 +105,17 @@ bzr_status bzr_sync(bzr_ctx *ctx);
 
 /* ---- measurement: per-kernel HIP-event timing on the context's stream ---- */
 enum {
-  BZR_KERNEL_TRAVERSE = 0,        /* BVH candidate search */
-  BZR_KERNEL_RESOLVE_HITS = 1,    /* Newton stage -> BezierIntersection */
-  BZR_KERNEL_RESOLVE_REFRACT = 2, /* Newton stage + refraction */
-  BZR_KERNEL_INTERSECT_SCAN = 3,  /* brute force (BZR_ACCEL_NONE) */
-  BZR_KERNEL_REFRACT_SCAN = 4,
-  BZR_KERNEL_CHAIN_SCAN = 5,
-  BZR_KERNEL_PATCH = 6,
-  BZR_KERNEL_COUNT = 7
+  BZR_KERNEL_TRAVERSE = 0,        /* BVH walk + planar gate -> candidate pairs, per-patch histogram */
+  BZR_KERNEL_BUCKET = 1,          /* prefix sum + scatter of the pairs into patch-major order */
+  BZR_KERNEL_NEWTON = 2,          /* Newton stage per pair, patch-uniform waves */
+  BZR_KERNEL_FOLLOW = 3,          /* follow-side neighbour retries */
+  BZR_KERNEL_FINISH = 4,          /* winner -> BezierIntersection / refraction */
+  BZR_KERNEL_OVERFLOW = 5,        /* in-order full scan for rays the culling cannot take */
+  BZR_KERNEL_INTERSECT_SCAN = 6,  /* brute force (BZR_ACCEL_NONE) */
+  BZR_KERNEL_REFRACT_SCAN = 7,
+  BZR_KERNEL_CHAIN_SCAN = 8,
+  BZR_KERNEL_PATCH = 9,
+  BZR_KERNEL_COUNT = 10
 };
 /* While enabled, every launch is bracketed by hipEvents on the context's stream. */
 bzr_status bzr_ctx_timing(bzr_ctx *ctx, int32_t enable);
