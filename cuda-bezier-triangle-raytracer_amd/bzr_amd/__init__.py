@@ -22,7 +22,8 @@ from pathlib import Path
 import numpy as np
 
 PKG_DIR = Path(__file__).resolve().parent.parent
-LIB_PATH = PKG_DIR / "lib" / "libbzr.so"
+# BZR_LIBRARY: an alternative build of libbzr.so (A/B experiments); default: the in-tree build
+LIB_PATH = Path(os.environ.get("BZR_LIBRARY", PKG_DIR / "lib" / "libbzr.so"))
 
 OK = 0
 HOST_PTRS, DEVICE_PTRS = 0, 1

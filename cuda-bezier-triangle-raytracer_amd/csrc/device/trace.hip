@@ -61,9 +61,8 @@ struct bzr_mesh {
   uint32_t n;
   float4 *planar;   // 4 float4 per patch: n.xyz c | hin hout M00 M01 | M02 M10 M11 M12 | M20 M21 M22 0
   float *full;      // 66 words per patch (bzr_patch)
-  bzr_host::BvhNode *nodes;
-  uint32_t *order;  // BVH leaf slots -> patch index
-  float4 *pbox;     // 2 float4 per BVH leaf slot: lo, hi of the patch's gate-region box
+  bzr_host::Bvh4Node *nodes;  // 4-wide BVH over the patches' gate-region boxes (bvh.cpp)
+  float4 *leaf;     // 4 float4 per BVH leaf slot: the planar record, patch index in the last word
   uint32_t nnodes;
   float s_max;
 };
@@ -92,16 +91,15 @@ namespace {
 constexpr int kBlock = 256;
 constexpr int kWaves = kBlock / 64;
 constexpr uint32_t kMaxLenses = 8;
-constexpr uint32_t kMaxCand = 8;         // candidate list length per ray and segment
+constexpr uint32_t kMaxCand = 16;        // candidate list length per ray and segment
 constexpr uint32_t kOverflow = 0xFFFFu;  // count value: resolve with the full scan
 constexpr int kStack = 64;
 
 struct MeshView {
   const float4 *__restrict__ planar;
   const float *__restrict__ full;
-  const bzr_host::BvhNode *__restrict__ nodes;
-  const uint32_t *__restrict__ order;
-  const float4 *__restrict__ pbox;
+  const bzr_host::Bvh4Node *__restrict__ nodes;
+  const float4 *__restrict__ leaf;
   uint32_t n;
   float s_max;
   float ri;
@@ -268,7 +266,7 @@ struct Work {
   uint32_t *count;   // [n]
   unsigned long long *key;  // [n]
   float *slot;       // [kSlotWords][cap] per-pair hit
-  uint2 *pairs;      // [cap] (ray, patch)
+  float4 *pairs;     // [2][cap] pair records: (s.xyz, ray) and (d.xyz, patch) -- the ray travels with the pair
   uint32_t *fol;     // [cap] pair | what << 30
   uint32_t *ovf;     // [n]
   void *cub;
@@ -362,29 +360,33 @@ __global__ __launch_bounds__(kBlock) void k_traverse(MeshView m, const float *__
     sp = 1;
   }
   while (sp > 0) {
-    uint32_t node = __builtin_amdgcn_readfirstlane(stack[wv][--sp]);
-    const bzr_host::BvhNode nd = m.nodes[node];
-    bool hit = active && slab(make_float4(nd.lo[0], nd.lo[1], nd.lo[2], 0.0f),
-                              make_float4(nd.hi[0], nd.hi[1], nd.hi[2], 0.0f), s, inv);
-    if (!__any(hit)) continue;
-    if (nd.b & bzr_host::kLeafFlag) {
-      uint32_t first = nd.a, num = nd.b & ~bzr_host::kLeafFlag;
-      for (uint32_t k = first; k < first + num; ++k) {
-        bool h2 = hit && slab(m.pbox[2 * k], m.pbox[2 * k + 1], s, inv);
-        if (!__any(h2)) continue;
-        uint32_t b = m.order[k];
-        const float4 *q = m.planar + 4u * b;
-        if (h2 && planar_gate(q[0], q[1], q[2], q[3], s, d)) {
-          if (cnt < kMaxCand) w.cand[(size_t)cnt * n + i] = b;
+    const uint32_t node = __builtin_amdgcn_readfirstlane(stack[wv][--sp]);
+    // wave-uniform record read through the constant address space: scalar loads into SGPRs
+    const __attribute__((address_space(4))) bzr_host::Bvh4Node &nd =
+        *((const __attribute__((address_space(4))) bzr_host::Bvh4Node *)(uintptr_t)m.nodes + node);
+    bool hit[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      hit[c] = active && nd.child[c] != bzr_host::kEmptyChild &&
+               slab(make_float4(nd.lo[0][c], nd.lo[1][c], nd.lo[2][c], 0.0f),
+                    make_float4(nd.hi[0][c], nd.hi[1][c], nd.hi[2][c], 0.0f), s, inv);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      if (!__any(hit[c])) continue;
+      const uint32_t ch = nd.child[c];
+      if (ch & bzr_host::kLeafFlag) {
+        const const_float *q = (const const_float *)(uintptr_t)m.leaf + 16u * (ch & ~bzr_host::kLeafFlag);
+        const float4 q0 = make_float4(q[0], q[1], q[2], q[3]), q1 = make_float4(q[4], q[5], q[6], q[7]);
+        const float4 q2 = make_float4(q[8], q[9], q[10], q[11]), q3 = make_float4(q[12], q[13], q[14], q[15]);
+        if (hit[c] && planar_gate(q0, q1, q2, q3, s, d)) {
+          if (cnt < kMaxCand) w.cand[(size_t)cnt * n + i] = __float_as_uint(q3.w);
           cnt = cnt < kMaxCand ? cnt + 1 : kOverflow;
         }
+      } else if (sp < kStack) {
+        stack[wv][sp++] = ch;
+      } else {  // traversal stack exhausted: resolve these rays with the full scan
+        if (hit[c]) cnt = kOverflow;
       }
-    } else if (sp + 2 <= kStack) {
-      stack[wv][sp] = nd.b;
-      stack[wv][sp + 1] = nd.a;
-      sp += 2;
-    } else {  // traversal stack exhausted: resolve these rays with the full scan
-      if (hit) cnt = kOverflow;
     }
   }
   if (i >= n) return;
@@ -392,85 +394,133 @@ __global__ __launch_bounds__(kBlock) void k_traverse(MeshView m, const float *__
   w.key[i] = ~0ull;
   if (cnt > kMaxCand) w.ovf[atomicAdd(&w.ctr[1], 1u)] = i;
   // Rank of each (ray, patch) pair within its patch bucket.  Neighbouring rays mostly share
-  // patches, so the lanes of a wave that name the same patch take one atomicAdd together.
+  // patches: the lanes naming the same patch form a group (found with ballots, no memory traffic),
+  // each group's first lane adds the group size -- all groups in one atomic instruction -- and the
+  // lanes take their rank from the returned base.
+  const uint32_t lane = threadIdx.x & 63u;
   const uint32_t listed = cnt <= kMaxCand ? cnt : 0u;
   for (uint32_t j = 0; __any(j < listed); ++j) {
-    bool pend = j < listed;
+    const bool pend = j < listed;
     const uint32_t b = pend ? w.cand[(size_t)j * n + i] : 0u;
+    unsigned long long group = 0ull;
+    bool todo = pend;
     for (;;) {
-      const unsigned long long mask = __ballot(pend);
+      const unsigned long long mask = __ballot(todo);
       if (mask == 0ull) break;
       const uint32_t b0 = __builtin_amdgcn_readlane(b, __builtin_ctzll(mask));
-      const bool same = pend && b == b0;
-      const unsigned long long group = __ballot(same);
-      const uint32_t leader = __builtin_ctzll(group);
-      uint32_t base = 0;
-      if ((threadIdx.x & 63u) == leader) base = atomicAdd(&w.hist[b0], (uint32_t)__popcll(group));
-      base = __builtin_amdgcn_readlane(base, leader);
+      const bool same = todo && b == b0;
+      const unsigned long long g = __ballot(same);
       if (same) {
-        w.rank[(size_t)j * n + i] = base + lanes_below(group);
-        pend = false;
+        group = g;
+        todo = false;
       }
     }
+    const uint32_t leader = pend ? (uint32_t)__builtin_ctzll(group) : lane;
+    uint32_t base = 0;
+    if (pend && lane == leader) base = atomicAdd(&w.hist[b], (uint32_t)__popcll(group));
+    base = __shfl(base, (int)leader, 64);
+    if (pend) w.rank[(size_t)j * n + i] = base + lanes_below(group);
   }
 }
 
-__global__ __launch_bounds__(kBlock) void k_scatter(uint32_t n, Work w) {
+__global__ __launch_bounds__(kBlock) void k_scatter(const float *__restrict__ rays, uint32_t ld, uint32_t off,
+                                                    uint32_t n, Work w) {
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
   uint32_t c = w.count[i];
-  if (c > kMaxCand) return;
+  if (c > kMaxCand || c == 0) return;
+  f3 s, d;
+  load_ray(rays, ld, off + i, s, d);
   for (uint32_t j = 0; j < c; ++j) {
-    uint32_t b = w.cand[(size_t)j * n + i];
-    w.pairs[w.offs[b] + w.rank[(size_t)j * n + i]] = make_uint2(i, b);
+    const uint32_t b = w.cand[(size_t)j * n + i];
+    const uint32_t p = w.offs[b] + w.rank[(size_t)j * n + i];
+    w.pairs[p] = make_float4(s.x, s.y, s.z, __uint_as_float(i));
+    w.pairs[(size_t)w.cap + p] = make_float4(d.x, d.y, d.z, __uint_as_float(b));
   }
 }
 
-// `full` is a separate __restrict__ argument (noalias: the kernel's stores cannot clobber it), so the
-// wave-uniform patch record below is fetched with scalar loads into SGPRs.
-__global__ __launch_bounds__(kBlock) void k_newton(const float *__restrict__ full, const float *__restrict__ rays,
-                                                   uint32_t ld, uint32_t off, const uint32_t *__restrict__ total,
-                                                   const uint2 *__restrict__ pairs, float *__restrict__ slot,
+constexpr uint32_t kFolBuf = 256;  // per-wave LDS staging of follow requests
+
+// Copies a wave's staged follow requests to the global list (one atomicAdd for all of them).
+__device__ __forceinline__ void flush_follow(uint32_t *buf, uint32_t &nf, uint32_t *__restrict__ fol,
+                                             uint32_t *__restrict__ nfol, uint32_t lane) {
+  uint32_t base = 0;
+  if (lane == 0) base = atomicAdd(nfol, nf);
+  base = __builtin_amdgcn_readfirstlane(base);
+  for (uint32_t k = lane; k < nf; k += 64u) fol[base + k] = buf[k];
+  nf = 0;
+}
+
+// Persistent waves: wave g takes 64-pair chunks g, g + W, ... and fetches the next chunk's pair
+// records while it computes the current one.  A chunk holds few distinct patches (buckets are
+// contiguous); each is processed with its record in scalar registers, `full` being a __restrict__
+// constant-address-space read.
+__global__ __launch_bounds__(kBlock) void k_newton(const float *__restrict__ full, const uint32_t *__restrict__ total,
+                                                   const float4 *__restrict__ pairs, float *__restrict__ slot,
                                                    uint32_t cap, unsigned long long *__restrict__ key,
                                                    uint32_t *__restrict__ fol, uint32_t *__restrict__ nfol) {
+  __shared__ uint32_t fbuf[kWaves][kFolBuf];
+  const uint32_t wv = threadIdx.x >> 6;
+  uint32_t nf = 0;  // staged follow requests of this wave (uniform)
   const uint32_t P = __builtin_amdgcn_readfirstlane(*total);
-  for (uint32_t base = blockIdx.x * kBlock; base < P; base += gridDim.x * kBlock) {
-    const uint32_t p = base + threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t nchunks = (P + 63u) / 64u;
+  const uint32_t W = gridDim.x * kWaves;
+  uint32_t q = blockIdx.x * kWaves + (threadIdx.x >> 6);
+  float4 a = make_float4(0.0f, 0.0f, 0.0f, 0.0f), e = a;
+  if (q < nchunks && q * 64u + lane < P) {
+    a = pairs[q * 64u + lane];
+    e = pairs[(size_t)cap + q * 64u + lane];
+  }
+  for (; q < nchunks; q += W) {
+    const uint32_t p = q * 64u + lane;
     bool todo = p < P;
-    uint2 pr = todo ? pairs[p] : make_uint2(0u, 0u);
-    f3 s = mk(0.0f, 0.0f, 0.0f), d = s;
-    if (todo) load_ray(rays, ld, off + pr.x, s, d);
+    const f3 s = mk(a.x, a.y, a.z), d = mk(e.x, e.y, e.z);
+    const uint32_t ray = __float_as_uint(a.w), b = __float_as_uint(e.w);
+    const uint32_t qn = q + W, pn = qn * 64u + lane;  // prefetch the next chunk
+    if (qn < nchunks && pn < P) {
+      a = pairs[pn];
+      e = pairs[(size_t)cap + pn];
+    }
+    bool is_fol = false;
+    uint32_t fol_entry = 0;
     for (;;) {
-      unsigned long long mask = __ballot(todo);
+      const unsigned long long mask = __ballot(todo);
       if (mask == 0ull) break;
-      // the next patch of this wave, wave-uniform: its record is fetched with scalar loads
-      const uint32_t b0 = __builtin_amdgcn_readlane(pr.y, __builtin_ctzll(mask));
-      // fetched before the branch: inside it the compiler would substitute the per-lane pr.y for b0
-      const Patch pa = load_patch_uniform(full, b0);
-      if (todo && pr.y == b0) {
+      // the next patch of this chunk, wave-uniform: its record is fetched with scalar loads
+      const uint32_t b0 = __builtin_amdgcn_readlane(b, __builtin_ctzll(mask));
+      // formed before the branch: inside it the compiler would substitute the per-lane b for b0
+      const auto pa = uniform_patch(full, b0);
+      if (todo && b == b0) {
         todo = false;
-        Hit h = patch_intersect(pa, s, d, false);
-        if (h.what <= kFollow2)
-          fol[atomicAdd(nfol, 1u)] = p | (h.what << 30);
-        else if (h.what == kIntersect)
-          record(slot, cap, p, h, b0, &key[pr.x]);
+        const Hit h = patch_intersect(pa, s, d, false);
+        if (h.what == kIntersect) record(slot, cap, p, h, b0, &key[ray]);
+        is_fol = h.what <= kFollow2;
+        fol_entry = p | (h.what << 30);
       }
     }
+    // follow requests: staged in this wave's LDS buffer, published with one atomic per flush
+    const unsigned long long fm = __ballot(is_fol);
+    if (fm) {
+      if (is_fol) fbuf[wv][nf + lanes_below(fm)] = fol_entry;
+      nf += (uint32_t)__popcll(fm);
+      if (nf > kFolBuf - 64u) flush_follow(fbuf[wv], nf, fol, nfol, lane);
+    }
   }
+  if (nf) flush_follow(fbuf[wv], nf, fol, nfol, lane);
 }
 
 __global__ __launch_bounds__(kBlock) void k_follow(MeshView m, const float *__restrict__ rays, uint32_t ld,
                                                    uint32_t off, Work w) {
   const uint32_t F = __builtin_amdgcn_readfirstlane(w.ctr[0]);
   for (uint32_t q = blockIdx.x * kBlock + threadIdx.x; q < F; q += gridDim.x * kBlock) {
-    const uint32_t e = w.fol[q], p = e & 0x3FFFFFFFu, what = e >> 30;
-    const uint2 pr = w.pairs[p];
-    f3 s, d;
-    load_ray(rays, ld, off + pr.x, s, d);
-    const uint32_t nbr = __float_as_uint(m.full[(size_t)rec::kWords * pr.y + rec::kNeigh + what]);
+    const uint32_t f = w.fol[q], p = f & 0x3FFFFFFFu, what = f >> 30;
+    const float4 a = w.pairs[p], e = w.pairs[(size_t)w.cap + p];
+    const f3 s = mk(a.x, a.y, a.z), d = mk(e.x, e.y, e.z);
+    const uint32_t nbr = __float_as_uint(m.full[(size_t)rec::kWords * __float_as_uint(e.w) + rec::kNeigh + what]);
     Patch pa = load_patch(m.full + (size_t)rec::kWords * nbr);
     Hit h = patch_intersect(pa, s, d, true);
-    if (h.what == kIntersect) record(w.slot, w.cap, p, h, nbr, &w.key[pr.x]);
+    if (h.what == kIntersect) record(w.slot, w.cap, p, h, nbr, &w.key[__float_as_uint(a.w)]);
   }
 }
 
@@ -501,9 +551,9 @@ __global__ __launch_bounds__(kBlock) void k_finish(const float *rays, uint32_t l
   emit<kMode>(o, ld, gi, s, d, h, patch);
 }
 
-// The rays k_traverse could not take, one wave per ray: lane l scans patches l, l+64, ... in index
-// order (strict <, so per lane the lowest index wins ties), then the wave takes the (t, index)
-// lexicographic minimum -- the winner of the reference's single in-order scan.
+// The rays k_traverse could not take, one block per ray: thread t scans patches t, t+256, ... in
+// index order (strict <, so per thread the lowest index wins ties), then the block takes the
+// (t, index) lexicographic minimum -- the winner of the reference's single in-order scan.
 __device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v) {
 #pragma unroll
   for (int k = 32; k >= 1; k >>= 1) {
@@ -516,16 +566,16 @@ __device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v)
 template <int kMode>
 __global__ __launch_bounds__(kBlock) void k_overflow(MeshView m, const float *rays, uint32_t ld, uint32_t off, Work w,
                                                      Out o) {
+  __shared__ unsigned long long red[kWaves];
   const uint32_t V = __builtin_amdgcn_readfirstlane(w.ctr[1]);
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t nwaves = gridDim.x * kWaves;
-  for (uint32_t q = blockIdx.x * kWaves + (threadIdx.x >> 6); q < V; q += nwaves) {
+  for (uint32_t q = blockIdx.x; q < V; q += gridDim.x) {
     const uint32_t gi = off + w.ovf[q];
     f3 s, d;
     load_ray(rays, ld, gi, s, d);
     Hit best = no_hit();
     uint32_t best_b = 0xFFFFFFFFu, best_src = 0xFFFFFFFFu;
-    for (uint32_t b = lane; b < m.n; b += 64u) {
+#pragma unroll 4
+    for (uint32_t b = threadIdx.x; b < m.n; b += kBlock) {
       const float4 *qq = m.planar + 4u * b;
       if (!planar_gate(qq[0], qq[1], qq[2], qq[3], s, d)) continue;
       uint32_t src;
@@ -538,9 +588,14 @@ __global__ __launch_bounds__(kBlock) void k_overflow(MeshView m, const float *ra
     }
     const unsigned long long mine =
         best_b != 0xFFFFFFFFu ? ((unsigned long long)t_order(best.t) << 32) | best_b : ~0ull;
-    const unsigned long long win = wave_min_u64(mine);
+    unsigned long long win = wave_min_u64(mine);
+    if ((threadIdx.x & 63u) == 0) red[threadIdx.x >> 6] = win;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kWaves; ++k) win = red[k] < win ? red[k] : win;
+    __syncthreads();  // red is reused by the next ray
     if (win == ~0ull) {
-      if (lane == 0) emit<kMode>(o, ld, gi, s, d, no_hit(), 0xFFFFFFFFu);
+      if (threadIdx.x == 0) emit<kMode>(o, ld, gi, s, d, no_hit(), 0xFFFFFFFFu);
     } else if (mine == win) {
       emit<kMode>(o, ld, gi, s, d, best, best_src);
     }
@@ -644,7 +699,7 @@ struct DeviceGuard {
 };
 
 MeshView view_of(const bzr_mesh *m, float ri = 1.0f) {
-  return MeshView{m->planar, m->full, m->nodes, m->order, m->pbox, m->n, m->s_max, ri};
+  return MeshView{m->planar, m->full, m->nodes, m->leaf, m->n, m->s_max, ri};
 }
 unsigned grid_for(uint32_t n) { return (n + kBlock - 1) / kBlock; }
 size_t round256(size_t b) { return (b + 255) & ~size_t(255); }
@@ -726,6 +781,21 @@ struct Span {
   }
 };
 
+// Blocks of `kernel` (kBlock threads) the device holds at once: the persistent-grid size.
+template <typename K>
+uint32_t resident_blocks(bzr_ctx *ctx, K kernel) {
+  static thread_local std::vector<std::pair<const void *, uint32_t>> cache;  // (kernel, blocks) per device below
+  const void *key = reinterpret_cast<const void *>(kernel);
+  for (auto const &c : cache)
+    if (c.first == key) return c.second;
+  int per_cu = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, 0) != hipSuccess || per_cu < 1) per_cu = 1;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess || cus < 1) cus = 256;
+  uint32_t blocks = static_cast<uint32_t>(per_cu) * static_cast<uint32_t>(cus);
+  cache.emplace_back(key, blocks);
+  return blocks;
+}
+
 // Workspace of the culled path for chunks of up to `chunk` rays over meshes of up to `nb` patches.
 bzr_status ensure_work(bzr_ctx *ctx, uint32_t chunk, uint32_t nb, Work &w) {
   size_t cub_bytes = 0;
@@ -734,7 +804,7 @@ bzr_status ensure_work(bzr_ctx *ctx, uint32_t chunk, uint32_t nb, Work &w) {
   const size_t cap = (size_t)kMaxCand * chunk;
   const size_t bytes = round256((size_t)(nb + 5) * 4) + round256((size_t)(nb + 1) * 4) + 2 * round256(cap * 4) +
                        round256((size_t)chunk * 4) + round256((size_t)chunk * 8) + round256(kSlotWords * cap * 4) +
-                       round256(cap * 8) + round256(cap * 4) + round256((size_t)chunk * 4) + round256(cub_bytes);
+                       round256(cap * 32) + round256(cap * 4) + round256((size_t)chunk * 4) + round256(cub_bytes);
   if (bzr_status s = ensure_buffer(ctx->work, ctx->work_bytes, bytes)) return s;
   Staging st{static_cast<char *>(ctx->work)};
   w.hist = st.take<uint32_t>(nb + 5);
@@ -745,7 +815,7 @@ bzr_status ensure_work(bzr_ctx *ctx, uint32_t chunk, uint32_t nb, Work &w) {
   w.count = st.take<uint32_t>(chunk);
   w.key = st.take<unsigned long long>(chunk);
   w.slot = st.take<float>(kSlotWords * cap);
-  w.pairs = st.take<uint2>(cap);
+  w.pairs = st.take<float4>(2 * cap);
   w.fol = st.take<uint32_t>(cap);
   w.ovf = st.take<uint32_t>(chunk);
   w.cub = st.take<char>(cub_bytes ? cub_bytes : 1);
@@ -754,8 +824,8 @@ bzr_status ensure_work(bzr_ctx *ctx, uint32_t chunk, uint32_t nb, Work &w) {
   return BZR_OK;
 }
 
-// Chunk size of the culled path: bounds the workspace (~560 B per ray) for very large batches.
-constexpr uint32_t kChunk = 1u << 22;
+// Chunk size of the culled path: bounds the workspace (~1.5 KB per ray) for very large batches.
+constexpr uint32_t kChunk = 1u << 20;
 uint32_t chunk_for(uint32_t n) { return n < kChunk ? n : kChunk; }
 
 // One BezierMesh::intersect per ray of rays [off, off + n) (+ refraction, per kMode).
@@ -768,16 +838,17 @@ bzr_status run_culled(bzr_ctx *ctx, const MeshView &mv, const float *rays, uint3
   {
     Span sp(ctx, BZR_KERNEL_BUCKET);
     BZR_HIP(hipcub::DeviceScan::ExclusiveSum(w.cub, w.cub_bytes, w.hist, w.offs, nb + 1, ctx->stream));
-    launch(ctx, -1, k_scatter, dim3(grid_for(n)), n, w);
+    launch(ctx, -1, k_scatter, dim3(grid_for(n)), rays, ld, off, n, w);
   }
-  const uint32_t gn = std::min<uint32_t>(std::max<uint32_t>(grid_for(2 * n), 1u), 16384u);
-  launch(ctx, BZR_KERNEL_NEWTON, k_newton, dim3(gn), mv.full, rays, ld, off, w.offs + nb, w.pairs, w.slot, w.cap, w.key,
-         w.fol, w.ctr);
+  // persistent grid: the resident capacity of the device, never more than the worst-case chunk count
+  const uint32_t gn = std::min<uint32_t>(std::max<uint32_t>((kMaxCand * n + kBlock - 1) / kBlock, 1u),
+                                         resident_blocks(ctx, k_newton));
+  launch(ctx, BZR_KERNEL_NEWTON, k_newton, dim3(gn), mv.full, w.offs + nb, w.pairs, w.slot, w.cap, w.key, w.fol,
+         w.ctr);
   launch(ctx, BZR_KERNEL_FOLLOW, k_follow, dim3(std::min<uint32_t>(grid_for(n / 8 + 1), 1024u)), mv, rays, ld, off,
          w);
   launch(ctx, BZR_KERNEL_FINISH, k_finish<kMode>, dim3(grid_for(n)), rays, ld, off, n, w, o);
-  launch(ctx, BZR_KERNEL_OVERFLOW, k_overflow<kMode>, dim3(std::min<uint32_t>((n + kWaves - 1) / kWaves, 2048u)), mv,
-         rays, ld, off, w, o);
+  launch(ctx, BZR_KERNEL_OVERFLOW, k_overflow<kMode>, dim3(std::min<uint32_t>(n, 2048u)), mv, rays, ld, off, w, o);
   BZR_HIP(hipGetLastError());
   return BZR_OK;
 }
@@ -890,7 +961,7 @@ extern "C" bzr_status bzr_mesh_create(bzr_ctx *ctx, const void *patches, uint32_
   if (stride < sizeof(bzr_patch)) return set_error(BZR_ERR_INVALID_ARGUMENT, "stride smaller than bzr_patch");
   *out = nullptr;
   DeviceGuard g(ctx->device);
-  std::vector<float> full((size_t)n * rec::kWords);
+  std::vector<float> full((size_t)n * rec::kWords);  // index order
   std::vector<float4> planar((size_t)n * 4);
   const char *src = static_cast<const char *>(patches);
   for (uint32_t i = 0; i < n; ++i) {
@@ -908,15 +979,17 @@ extern "C" bzr_status bzr_mesh_create(bzr_ctx *ctx, const void *patches, uint32_
   } catch (std::exception const &e) {
     return set_error(BZR_ERR_OUT_OF_MEMORY, std::string("BVH build: ") + e.what());
   }
-  if (bvh.nodes.empty()) {  // empty mesh: a root that nothing hits
-    bzr_host::BvhNode root{{1, 1, 1}, 0, {0, 0, 0}, bzr_host::kLeafFlag};
-    bvh.nodes.push_back(root);
+  std::vector<float4> leaf((size_t)n * 4);  // BVH slot order, patch index in the last word
+  for (uint32_t k = 0; k < n; ++k) {
+    uint32_t b = bvh.order[k];
+    for (int j = 0; j < 4; ++j) leaf[4 * k + j] = planar[4 * b + j];
+    std::memcpy(&leaf[4 * k + 3].w, &b, 4);
   }
   bzr_mesh *mesh = new (std::nothrow) bzr_mesh();
   if (!mesh) return set_error(BZR_ERR_OUT_OF_MEMORY, "mesh allocation");
   mesh->device = ctx->device;
   mesh->n = n;
-  mesh->nnodes = static_cast<uint32_t>(bvh.nodes.size());
+  mesh->nnodes = static_cast<uint32_t>(bvh.nodes4.size());
   mesh->s_max = bvh.s_max;
   struct Up {
     void **dst;
@@ -925,9 +998,8 @@ extern "C" bzr_status bzr_mesh_create(bzr_ctx *ctx, const void *patches, uint32_
   } ups[] = {
       {reinterpret_cast<void **>(&mesh->planar), planar.data(), planar.size() * sizeof(float4)},
       {reinterpret_cast<void **>(&mesh->full), full.data(), full.size() * sizeof(float)},
-      {reinterpret_cast<void **>(&mesh->nodes), bvh.nodes.data(), bvh.nodes.size() * sizeof(bzr_host::BvhNode)},
-      {reinterpret_cast<void **>(&mesh->order), bvh.order.data(), bvh.order.size() * sizeof(uint32_t)},
-      {reinterpret_cast<void **>(&mesh->pbox), bvh.patch_box.data(), bvh.patch_box.size() * sizeof(float)},
+      {reinterpret_cast<void **>(&mesh->nodes), bvh.nodes4.data(), bvh.nodes4.size() * sizeof(bzr_host::Bvh4Node)},
+      {reinterpret_cast<void **>(&mesh->leaf), leaf.data(), leaf.size() * sizeof(float4)},
   };
   hipError_t e = hipSuccess;
   for (auto &u : ups) {
@@ -951,8 +1023,7 @@ extern "C" bzr_status bzr_mesh_destroy(bzr_mesh *mesh) {
   (void)hipFree(mesh->planar);
   (void)hipFree(mesh->full);
   (void)hipFree(mesh->nodes);
-  (void)hipFree(mesh->order);
-  (void)hipFree(mesh->pbox);
+  (void)hipFree(mesh->leaf);
   delete mesh;
   return BZR_OK;
 }

@@ -165,7 +165,7 @@ struct Builder {
     BvhNode nd;
     std::memcpy(nd.lo, bb.lo.data(), 12);
     std::memcpy(nd.hi, bb.hi.data(), 12);
-    if (count <= kLeafSize) {
+    if (count <= 1) {
       nd.a = first;
       nd.b = kLeafFlag | count;
       nodes[id] = nd;
@@ -187,6 +187,57 @@ struct Builder {
     return id;
   }
 };
+
+bool box_empty(BvhNode const &nd) { return !(nd.lo[0] <= nd.hi[0] && nd.lo[1] <= nd.hi[1] && nd.lo[2] <= nd.hi[2]); }
+
+double half_area(BvhNode const &nd) {
+  double e[3];
+  for (int a = 0; a < 3; ++a) e[a] = std::max(0.0, (double)nd.hi[a] - (double)nd.lo[a]);
+  return e[0] * e[1] + e[1] * e[2] + e[2] * e[0];
+}
+
+// Collapse the binary tree under `n2` into 4-wide nodes: repeatedly open the child with the largest
+// box until four children remain.  Subtrees with empty boxes (no patch whose gate can pass) drop out.
+uint32_t collapse(std::vector<BvhNode> const &bin, uint32_t n2, std::vector<Bvh4Node> &out) {
+  uint32_t id = static_cast<uint32_t>(out.size());
+  out.push_back({});
+  std::vector<uint32_t> kids;
+  if (bin[n2].b & kLeafFlag)
+    kids.push_back(n2);
+  else
+    kids = {bin[n2].a, bin[n2].b};
+  while (kids.size() < 4) {
+    int best = -1;
+    double area = -1.0;
+    for (int i = 0; i < (int)kids.size(); ++i) {
+      BvhNode const &k = bin[kids[i]];
+      if ((k.b & kLeafFlag) || box_empty(k)) continue;
+      double ar = half_area(k);
+      if (ar > area || std::isnan(ar)) {
+        area = ar;
+        best = i;
+      }
+    }
+    if (best < 0) break;
+    uint32_t x = kids[best];
+    kids.erase(kids.begin() + best);
+    kids.push_back(bin[x].a);
+    kids.push_back(bin[x].b);
+  }
+  Bvh4Node nd{};
+  for (int c = 0; c < 4; ++c) nd.child[c] = kEmptyChild;
+  for (int c = 0; c < (int)kids.size(); ++c) {
+    BvhNode const &k = bin[kids[c]];
+    if (box_empty(k)) continue;
+    for (int a = 0; a < 3; ++a) {
+      nd.lo[a][c] = k.lo[a];
+      nd.hi[a][c] = k.hi[a];
+    }
+    nd.child[c] = (k.b & kLeafFlag) ? (kLeafFlag | k.a) : collapse(bin, kids[c], out);
+  }
+  out[id] = nd;
+  return id;
+}
 
 }  // namespace
 
@@ -216,6 +267,13 @@ Bvh build_bvh(const float *records, uint32_t n, uint32_t stride_words) {
   out.order.resize(n);
   std::iota(out.order.begin(), out.order.end(), 0u);
   if (n) bld.build(0, n);
+  if (n) {
+    collapse(out.nodes, 0, out.nodes4);
+  } else {
+    Bvh4Node root{};
+    for (int c = 0; c < 4; ++c) root.child[c] = kEmptyChild;
+    out.nodes4.push_back(root);
+  }
   out.patch_box.resize((size_t)n * 8);
   for (uint32_t k = 0; k < n; ++k) {
     Box const &b = box[out.order[k]];
@@ -240,5 +298,69 @@ extern "C" int32_t bzr_debug_gate_boxes(const void *patches, uint32_t n, uint32_
     }
   }
   *s_max = bvh.s_max;
+  return 0;
+}
+
+namespace {
+float safe_inv_h(float x) { return 1.0f / (std::fabs(x) < 1e-20f ? std::copysign(1e-20f, x) : x); }
+// same operation order as the device slab() in trace.hip
+bool slab_h(const float lo[3], const float hi[3], const float s[3], const float inv[3]) {
+  float a[3], b[3];
+  for (int k = 0; k < 3; ++k) {
+    a[k] = (lo[k] - s[k]) * inv[k];
+    b[k] = (hi[k] - s[k]) * inv[k];
+  }
+  float tnear = std::fmax(std::fmax(std::fmin(a[0], b[0]), std::fmin(a[1], b[1])), std::fmin(a[2], b[2]));
+  float tfar = std::fmin(std::fmin(std::fmax(a[0], b[0]), std::fmax(a[1], b[1])), std::fmax(a[2], b[2]));
+  return tnear <= tfar && tfar >= 0.0f;
+}
+}  // namespace
+
+extern "C" int32_t bzr_debug_traverse(const void *patches, uint32_t n, uint32_t stride, const float *rays, uint32_t nr,
+                                      uint8_t *hits, uint64_t stats[4]) {
+  if ((!patches && n) || (!rays && nr) || !stats || stride % 4 || stride < 264) return 1;
+  bzr_host::Bvh bvh = bzr_host::build_bvh(static_cast<const float *>(patches), n, stride / 4);
+  for (int k = 0; k < 4; ++k) stats[k] = 0;
+  for (uint32_t w0 = 0; w0 < nr; w0 += 64) {
+    uint32_t lanes = std::min<uint32_t>(64, nr - w0);
+    float s[64][3], inv[64][3];
+    bool active[64];
+    for (uint32_t l = 0; l < lanes; ++l) {
+      uint32_t r = w0 + l;
+      for (int k = 0; k < 3; ++k) {
+        s[l][k] = rays[(size_t)k * nr + r];
+        inv[l][k] = safe_inv_h(rays[(size_t)(3 + k) * nr + r]);
+      }
+      active[l] = std::fmax(std::fmax(std::fabs(s[l][0]), std::fabs(s[l][1])), std::fabs(s[l][2])) <= bvh.s_max;
+    }
+    stats[3] += 1;
+    if (!n) continue;
+    std::vector<uint32_t> stack{0u};
+    while (!stack.empty()) {
+      uint32_t node = stack.back();
+      stack.pop_back();
+      stats[0] += 1;
+      bzr_host::Bvh4Node const &nd = bvh.nodes4[node];
+      for (int c = 0; c < 4; ++c) {
+        if (nd.child[c] == bzr_host::kEmptyChild) continue;
+        float lo[3] = {nd.lo[0][c], nd.lo[1][c], nd.lo[2][c]}, hi[3] = {nd.hi[0][c], nd.hi[1][c], nd.hi[2][c]};
+        bool any = false;
+        bool hit[64];
+        for (uint32_t l = 0; l < lanes; ++l) any |= (hit[l] = active[l] && slab_h(lo, hi, s[l], inv[l]));
+        if (!any) continue;
+        if (nd.child[c] & bzr_host::kLeafFlag) {
+          uint32_t b = bvh.order[nd.child[c] & ~bzr_host::kLeafFlag];
+          stats[1] += 1;
+          for (uint32_t l = 0; l < lanes; ++l)
+            if (hit[l]) {
+              stats[2] += 1;
+              if (hits) hits[(size_t)(w0 + l) * n + b] = 1;
+            }
+        } else {
+          stack.push_back(nd.child[c]);
+        }
+      }
+    }
+  }
   return 0;
 }

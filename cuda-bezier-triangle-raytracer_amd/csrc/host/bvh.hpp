@@ -6,7 +6,6 @@
 
 namespace bzr_host {
 
-constexpr uint32_t kLeafSize = 4;
 constexpr uint32_t kLeafFlag = 0x80000000u;
 
 struct Box {
@@ -22,8 +21,21 @@ struct BvhNode {
   uint32_t b;
 };
 
+// 4-wide node of the device BVH (128 bytes, read with scalar loads): the gate boxes of up to four
+// children, SoA by coordinate.  child: inner node index, kLeafFlag | leaf slot (one patch), or
+// kEmptyChild (no child, or a subtree whose gate regions are all empty).
+constexpr uint32_t kEmptyChild = 0xFFFFFFFFu;
+struct Bvh4Node {
+  float lo[3][4];
+  float hi[3][4];
+  uint32_t child[4];
+  uint32_t pad[4];
+};
+static_assert(sizeof(Bvh4Node) == 128, "Bvh4Node layout");
+
 struct Bvh {
-  std::vector<BvhNode> nodes;      // root = 0
+  std::vector<Bvh4Node> nodes4;    // device BVH, root = 0 (always present)
+  std::vector<BvhNode> nodes;      // binary build tree (one patch per leaf), root = 0
   std::vector<uint32_t> order;     // leaf ranges index this: patch index in mesh order
   std::vector<float> patch_box;    // per order slot: lo.xyz, 0, hi.xyz, 0 (the gate-region box)
   float extent = 0.0f;             // max |coordinate| of any finite box

@@ -10,6 +10,13 @@ extern "C" {
 /* The culling boxes the BVH is built from, by patch index: boxes[6*i] = lo.xyz, hi.xyz of the region
  * where patch i's planar gate can pass for ray origins with |s|_inf <= *s_max.  Returns 0 on success. */
 int32_t bzr_debug_gate_boxes(const void *patches, uint32_t n, uint32_t stride, float *boxes, float *s_max);
+/* Host replay of the device BVH walk (same 4-wide tree, same float slab test) over `nr` rays in SoA
+ * [6, nr], grouped in waves of 64 consecutive rays.  hits (optional, nr x n bytes): hits[r*n + b] = 1
+ * when ray r reaches patch b's leaf box -- a superset of the patches whose planar gate it passes.
+ * stats[0] node visits (per wave), [1] leaf records fetched (per wave), [2] leaf-box hits (per ray),
+ * [3] waves.  Returns 0 on success. */
+int32_t bzr_debug_traverse(const void *patches, uint32_t n, uint32_t stride, const float *rays, uint32_t nr,
+                           uint8_t *hits, uint64_t stats[4]);
 #ifdef __cplusplus
 }
 #endif
