@@ -133,6 +133,12 @@ def main():
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
+    # work counters of one frame (device-side; measured here, outside the timed region)
+    ctx.counters(True)
+    ctx.counters_report()
+    step()
+    work_cnt = ctx.counters_report()
+    ctx.counters(False)
     seg_local = int(out_seg.sum().item())
     seg_total = torch.tensor([seg_local], dtype=torch.int64, device=dev)
     if world > 1:
@@ -166,12 +172,16 @@ def main():
         base, cnt = (None, None)
         if a.cpu_baseline == "on" and world == 1:
             base, cnt = cpu_baseline(cfg, side, patches, ris, a.cpu_sample_stride)
-        if cnt and cnt["segments"]:
-            newton_per_seg = cnt["newton"] / cnt["segments"]
-            follow_per_seg = cnt["follow"] / cnt["segments"]
-            tests_per_seg = cnt["tests"] / cnt["segments"]
-        else:  # SURVEY.md 8d measured values for cfg2
-            newton_per_seg, follow_per_seg, tests_per_seg = 1.258, 0.057, float(n_patch) / len(patches)
+        # measured on the GPU (bzr_ctx_counters, rank 0's frame); the brute-force-equivalent planar
+        # test count per segment is N_b (every patch), as SURVEY.md 8d prices it
+        segs = max(work_cnt["segments"], 1)
+        newton_per_seg = work_cnt["pairs"] / segs
+        follow_per_seg = work_cnt["follows"] / segs
+        tests_per_seg = float(n_patch) / len(patches)
+        if cnt and cnt["segments"]:  # cross-check with the oracle's counts on its sample
+            oracle_rates = {"newton": cnt["newton"] / cnt["segments"], "follow": cnt["follow"] / cnt["segments"]}
+        else:
+            oracle_rates = None
         # algorithmic work per step on rank 0: F_seg = 33 N_b + 1750 (N_cand + N_follow)
         seg_r0 = seg_local
         work = {
@@ -237,7 +247,10 @@ def main():
                 "hbm_achieved_GBps": round(alg_bytes / (chain_ms * 1e-3) / 1e9, 3),
                 "hbm_frac": round(alg_bytes / (chain_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 6),
                 "work_per_segment": {"planar_tests": round(tests_per_seg, 2), "newton": round(newton_per_seg, 4),
-                                     "follow": round(follow_per_seg, 4)},
+                                     "follow": round(follow_per_seg, 4),
+                                     "overflow_rays_per_frame": work_cnt["overflow_rays"],
+                                     "source": "GPU counters (bzr_ctx_counters)",
+                                     "oracle_sample_rates": oracle_rates},
             },
             "cpu_baseline": base,
         }

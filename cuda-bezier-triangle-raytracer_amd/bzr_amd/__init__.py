@@ -36,6 +36,7 @@ ENVELOPE_ELLIPSOID, ENVELOPE_TESTLENS = 0, 1
 PATCH_WORDS = 66  # sizeof(bzr_patch) / 4
 KERNELS = ("k_traverse", "bucket", "k_newton", "k_follow", "k_finish", "k_overflow", "k_intersect_scan",
            "k_refract_scan", "k_chain_scan", "k_patch")  # BZR_KERNEL_* ids
+COUNTERS = ("segments", "pairs", "follows", "overflow_rays")  # BZR_COUNTER_* ids
 HIT_FIELDS = 13
 
 _P = ctypes.c_void_p
@@ -56,6 +57,8 @@ _SIGS = {
     "bzr_sync": [_P],
     "bzr_ctx_timing": [_P, _I32],
     "bzr_ctx_timing_report": [_P, _P, _P],
+    "bzr_ctx_counters": [_P, _I32],
+    "bzr_ctx_counters_report": [_P, _P],
     "bzr_mesh_create": [_P, _P, _U32, _U32, ctypes.POINTER(_P)],
     "bzr_mesh_destroy": [_P],
     "bzr_mesh_size": [_P, ctypes.POINTER(_U32)],
@@ -206,6 +209,16 @@ class Context:
         calls = np.zeros(len(KERNELS), np.uint32)
         _check(lib().bzr_ctx_timing_report(self.handle, ms.ctypes.data, calls.ctypes.data))
         return {k: (float(ms[i]), int(calls[i])) for i, k in enumerate(KERNELS) if calls[i]}
+
+    def counters(self, enable: bool = True):
+        """Enable/disable the culled path's device work counters (see counters_report)."""
+        _check(lib().bzr_ctx_counters(self.handle, 1 if enable else 0))
+
+    def counters_report(self) -> dict:
+        """{segments, pairs, follows, overflow_rays} accumulated since the last report (synchronises)."""
+        out = np.zeros(len(COUNTERS), np.uint64)
+        _check(lib().bzr_ctx_counters_report(self.handle, out.ctypes.data))
+        return {k: int(out[i]) for i, k in enumerate(COUNTERS)}
 
     def close(self):
         if getattr(self, "handle", None):

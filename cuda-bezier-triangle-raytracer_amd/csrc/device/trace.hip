@@ -84,6 +84,8 @@ struct bzr_ctx {
   std::vector<hipEvent_t> spare; // event pool
   double ms[BZR_KERNEL_COUNT] = {};
   uint32_t calls[BZR_KERNEL_COUNT] = {};
+  bool counting = false;                 // work counters (bzr_ctx_counters)
+  unsigned long long *counters = nullptr;  // device [BZR_COUNTER_COUNT]
 };
 
 namespace {
@@ -259,7 +261,7 @@ __device__ __forceinline__ bool slab(float4 lo, float4 hi, f3 s, f3 inv) {
 // index): the atomicMin winner is the reference's strict-< in-order winner.
 struct Work {
   uint32_t *hist;    // [nb + 1] pair counts per patch (hist[nb] = 0), then ctr[4]
-  uint32_t *ctr;     // [0] follow count, [1] overflow count
+  uint32_t *ctr;     // [0] follow count, [1] overflow count, [2] rays traced
   uint32_t *offs;    // [nb + 1] exclusive prefix of hist; offs[nb] = pair count
   uint32_t *cand;    // [kMaxCand][n]
   uint32_t *rank;    // [kMaxCand][n]
@@ -340,7 +342,7 @@ __device__ __forceinline__ void record(float *__restrict__ slot, uint32_t cap, u
 // Candidate search.  `alive` (optional): a ray is traced iff alive[off + i] != BZR_RR_NONE.
 __global__ __launch_bounds__(kBlock) void k_traverse(MeshView m, const float *__restrict__ rays, uint32_t ld,
                                                      uint32_t off, const uint32_t *__restrict__ alive, uint32_t n,
-                                                     Work w) {
+                                                     Work w, uint32_t count_rays) {
   __shared__ uint32_t stack[kWaves][kStack];
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   const uint32_t wv = threadIdx.x >> 6;
@@ -388,6 +390,10 @@ __global__ __launch_bounds__(kBlock) void k_traverse(MeshView m, const float *__
         if (hit[c]) cnt = kOverflow;
       }
     }
+  }
+  if (count_rays) {  // rays traced (one atomic per wave: on one address, so only with counters on)
+    const unsigned long long traced = __ballot(i < n && (alive == nullptr || alive[off + i] != BZR_RR_NONE));
+    if ((threadIdx.x & 63u) == 0 && traced) atomicAdd(&w.ctr[2], (uint32_t)__popcll(traced));
   }
   if (i >= n) return;
   w.count[i] = cnt;
@@ -600,6 +606,14 @@ __global__ __launch_bounds__(kBlock) void k_overflow(MeshView m, const float *ra
       emit<kMode>(o, ld, gi, s, d, best, best_src);
     }
   }
+}
+
+__global__ void k_count(Work w, uint32_t nb, unsigned long long *__restrict__ counters) {
+  if (threadIdx.x != 0) return;
+  counters[BZR_COUNTER_SEGMENTS] += w.ctr[2];
+  counters[BZR_COUNTER_PAIRS] += w.offs[nb];
+  counters[BZR_COUNTER_FOLLOWS] += w.ctr[0];
+  counters[BZR_COUNTER_OVERFLOW_RAYS] += w.ctr[1];
 }
 
 __global__ void k_fill(uint32_t *__restrict__ a, uint32_t value, uint32_t n) {
@@ -834,7 +848,8 @@ bzr_status run_culled(bzr_ctx *ctx, const MeshView &mv, const float *rays, uint3
                       const uint32_t *alive, const Out &o, Work &w) {
   const uint32_t nb = mv.n;
   BZR_HIP(hipMemsetAsync(w.hist, 0, (size_t)(nb + 5) * 4, ctx->stream));
-  launch(ctx, BZR_KERNEL_TRAVERSE, k_traverse, dim3(grid_for(n)), mv, rays, ld, off, alive, n, w);
+  launch(ctx, BZR_KERNEL_TRAVERSE, k_traverse, dim3(grid_for(n)), mv, rays, ld, off, alive, n, w,
+         uint32_t(ctx->counting ? 1u : 0u));
   {
     Span sp(ctx, BZR_KERNEL_BUCKET);
     BZR_HIP(hipcub::DeviceScan::ExclusiveSum(w.cub, w.cub_bytes, w.hist, w.offs, nb + 1, ctx->stream));
@@ -849,6 +864,8 @@ bzr_status run_culled(bzr_ctx *ctx, const MeshView &mv, const float *rays, uint3
          w);
   launch(ctx, BZR_KERNEL_FINISH, k_finish<kMode>, dim3(grid_for(n)), rays, ld, off, n, w, o);
   launch(ctx, BZR_KERNEL_OVERFLOW, k_overflow<kMode>, dim3(std::min<uint32_t>(n, 2048u)), mv, rays, ld, off, w, o);
+  if (ctx->counting && ctx->counters)
+    hipLaunchKernelGGL(k_count, dim3(1), dim3(64), 0, ctx->stream, w, nb, ctx->counters);
   BZR_HIP(hipGetLastError());
   return BZR_OK;
 }
@@ -914,6 +931,30 @@ extern "C" bzr_status bzr_ctx_timing_report(bzr_ctx *ctx, float ms[BZR_KERNEL_CO
   return BZR_OK;
 }
 
+extern "C" bzr_status bzr_ctx_counters(bzr_ctx *ctx, int32_t enable) {
+  if (!ctx) return set_error(BZR_ERR_INVALID_ARGUMENT, "null context");
+  DeviceGuard g(ctx->device);
+  if (enable && !ctx->counters) {
+    BZR_HIP(hipMalloc(&ctx->counters, BZR_COUNTER_COUNT * sizeof(unsigned long long)));
+    BZR_HIP(hipMemsetAsync(ctx->counters, 0, BZR_COUNTER_COUNT * sizeof(unsigned long long), ctx->stream));
+  }
+  ctx->counting = enable != 0;
+  return BZR_OK;
+}
+
+extern "C" bzr_status bzr_ctx_counters_report(bzr_ctx *ctx, uint64_t counts[BZR_COUNTER_COUNT]) {
+  if (!ctx || !counts) return set_error(BZR_ERR_INVALID_ARGUMENT, "null argument");
+  for (int k = 0; k < BZR_COUNTER_COUNT; ++k) counts[k] = 0;
+  if (!ctx->counters) return BZR_OK;
+  DeviceGuard g(ctx->device);
+  unsigned long long host[BZR_COUNTER_COUNT];
+  BZR_HIP(hipMemcpyAsync(host, ctx->counters, sizeof(host), hipMemcpyDeviceToHost, ctx->stream));
+  BZR_HIP(hipMemsetAsync(ctx->counters, 0, sizeof(host), ctx->stream));
+  BZR_HIP(hipStreamSynchronize(ctx->stream));
+  for (int k = 0; k < BZR_COUNTER_COUNT; ++k) counts[k] = host[k];
+  return BZR_OK;
+}
+
 extern "C" bzr_status bzr_ctx_destroy(bzr_ctx *ctx) {
   if (!ctx) return BZR_OK;
   DeviceGuard g(ctx->device);
@@ -926,6 +967,7 @@ extern "C" bzr_status bzr_ctx_destroy(bzr_ctx *ctx) {
   for (auto e : ctx->spare) (void)hipEventDestroy(e);
   if (ctx->scratch) (void)hipFree(ctx->scratch);
   if (ctx->work) (void)hipFree(ctx->work);
+  if (ctx->counters) (void)hipFree(ctx->counters);
   (void)hipStreamDestroy(ctx->own);
   delete ctx;
   return BZR_OK;

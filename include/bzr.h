@@ -123,6 +123,19 @@ bzr_status bzr_ctx_timing(bzr_ctx *ctx, int32_t enable);
  * report, and resets them. */
 bzr_status bzr_ctx_timing_report(bzr_ctx *ctx, float ms[BZR_KERNEL_COUNT], uint32_t calls[BZR_KERNEL_COUNT]);
 
+/* ---- measurement: work counters of the culled path (device-side, accumulated per segment) ---- */
+enum {
+  BZR_COUNTER_SEGMENTS = 0,      /* rays traced (one BezierMesh::intersect each) */
+  BZR_COUNTER_PAIRS = 1,         /* (ray, patch) pairs that passed the planar gate: Newton runs */
+  BZR_COUNTER_FOLLOWS = 2,       /* follow-side retries on a neighbour patch: Newton runs */
+  BZR_COUNTER_OVERFLOW_RAYS = 3, /* rays resolved by the in-order full scan */
+  BZR_COUNTER_COUNT = 4
+};
+/* While enabled, each culled segment adds its counts on the device (one tiny kernel per segment). */
+bzr_status bzr_ctx_counters(bzr_ctx *ctx, int32_t enable);
+/* Synchronises, returns the counts accumulated since the last report, and resets them. */
+bzr_status bzr_ctx_counters_report(bzr_ctx *ctx, uint64_t counts[BZR_COUNTER_COUNT]);
+
 /* ---- device mesh: BezierMesh's patch vector (reference/bezierMesh.h:17) ---- */
 /* Copies n records of `stride` bytes (stride >= sizeof(bzr_patch)) from host memory. */
 bzr_status bzr_mesh_create(bzr_ctx *ctx, const void *patches, uint32_t n, uint32_t stride, bzr_mesh **out);

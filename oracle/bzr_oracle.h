@@ -20,8 +20,11 @@
  *   - the hot path (BezierTriangle::intersect / BezierMesh::intersect /
  *     BezierLens::refract) has NO known answer in the reference and the
  *     reference cannot be built here (Eigen3 absent, no network): hot-path
- *     parity against the reference itself is UNPINNED; it is cross-checked
- *     against the statistics SURVEY.md section 8 recorded from the reference.
+ *     parity against the reference itself is PARTIALLY PINNED -- by the
+ *     reference's refraction harness (reference/test.cpp:330-427, 22 inside /
+ *     22 outside events, tests/test_reference_harness.py) and the statistics
+ *     SURVEY.md section 8 recorded from the reference; the golden fixtures in
+ *     tests/golden/ are generated from this oracle (regression pins).
  *
  * Documented deviations from the reference (both are undefined behaviour there):
  *   D1  Plane::intersect(start, dir) (reference/3dGeomUtil.h:279-296) writes
