@@ -19,7 +19,7 @@ step() {  # step <name> <seconds> <cmd...>
 nproc > "$OUT/host.txt"; lscpu | grep -m1 "Model name" >> "$OUT/host.txt"
 for s in $STEPS; do
   case $s in
-    pytest) step pytest_gpu 900 python -m pytest tests -x -q -m gpu -p no:cacheprovider ;;
+    pytest) step pytest_gpu 900 python -u -m pytest tests -x -v -m gpu -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     smoke)  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)  step bench 600 python bench.py ${BENCH_ARGS:-} ;;
     prof)   (cd /tmp && export TMPDIR=/tmp && step prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run \
