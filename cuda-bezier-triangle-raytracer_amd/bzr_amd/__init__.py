@@ -35,8 +35,8 @@ RR_NONE, RR_INSIDE, RR_OUTSIDE = 0, 1, 2
 ENVELOPE_ELLIPSOID, ENVELOPE_TESTLENS = 0, 1
 PATCH_WORDS = 66  # sizeof(bzr_patch) / 4
 KERNELS = ("k_traverse", "bucket", "k_newton", "k_follow", "k_finish", "k_overflow", "k_intersect_scan",
-           "k_refract_scan", "k_chain_scan", "k_patch")  # BZR_KERNEL_* ids
-COUNTERS = ("segments", "pairs", "follows", "overflow_rays")  # BZR_COUNTER_* ids
+           "k_refract_scan", "k_chain_scan", "k_patch", "k_newton_lane")  # BZR_KERNEL_* ids
+COUNTERS = ("segments", "pairs", "follows", "overflow_rays", "lane_chunks")  # BZR_COUNTER_* ids
 HIT_FIELDS = 13
 
 _P = ctypes.c_void_p

@@ -199,7 +199,9 @@ struct Hit {
 constexpr uint32_t kFollow2 = 2u, kNone = 3u, kIntersect = 4u;
 
 // BezierTriangle::intersect (reference/bezierTriangle.cpp:123-195).  limitNone: 0 = cThis, 1 = cNone.
-template <typename P>
+// kGated: the caller has already evaluated the planar gate (:124-131) with this same arithmetic and
+// it passed (the culled pipeline's candidates), so its early returns are skipped -- same result bits.
+template <bool kGated = false, typename P>
 __device__ __forceinline__ Hit patch_intersect(const P &p, f3 s, f3 d, bool limitNone) {
   Hit h;
   h.t = 0.0f;
@@ -211,10 +213,12 @@ __device__ __forceinline__ Hit patch_intersect(const P &p, f3 s, f3 d, bool limi
   f3 ip;
   float ic, it;
   bool valid = plane_ray(p.n(), p.c(), s, d, ip, ic, it);
-  if (!(valid && fabsf(it) > -p.hin() && fabsf(it) > p.hout())) return h;
-  f3 b0 = matvec(p, ip);
-  if (!(limitNone || (b0.x >= 0.0f && b0.x <= 1.0f && b0.y >= 0.0f && b0.y <= 1.0f && b0.z >= 0.0f && b0.z <= 1.0f)))
-    return h;
+  if (!kGated) {
+    if (!(valid && fabsf(it) > -p.hin() && fabsf(it) > p.hout())) return h;
+    f3 b0 = matvec(p, ip);
+    if (!(limitNone || (b0.x >= 0.0f && b0.x <= 1.0f && b0.y >= 0.0f && b0.y <= 1.0f && b0.z >= 0.0f && b0.z <= 1.0f)))
+      return h;
+  }
   float din = div_rn(p.hin(), ic), dout = div_rn(p.hout(), ic);
   float closer = it + (ic > 0.0f ? din : dout);
   float further = it + (ic > 0.0f ? dout : din);

@@ -97,6 +97,19 @@ constexpr uint32_t kMaxCand = 16;        // candidate list length per ray and se
 constexpr uint32_t kOverflow = 0xFFFFu;  // count value: resolve with the full scan
 constexpr int kStack = 64;
 
+// 64-byte wave-uniform records read through the constant address space: one s_load_dwordx16 each
+typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(4))) const u32x16 cu32x16;
+
+// BZR_NEWTON_GATED (default 1): k_newton skips the planar gate its pairs already passed in k_traverse.
+#ifndef BZR_NEWTON_GATED
+#define BZR_NEWTON_GATED 1
+#endif
+// A 64-pair chunk with more distinct patches than this goes to k_newton_lane (one record per lane).
+#ifndef BZR_LANE_THRESHOLD
+#define BZR_LANE_THRESHOLD 3
+#endif
+constexpr uint32_t kLaneThreshold = BZR_LANE_THRESHOLD;
 struct MeshView {
   const float4 *__restrict__ planar;
   const float *__restrict__ full;
@@ -261,7 +274,7 @@ __device__ __forceinline__ bool slab(float4 lo, float4 hi, f3 s, f3 inv) {
 // index): the atomicMin winner is the reference's strict-< in-order winner.
 struct Work {
   uint32_t *hist;    // [nb + 1] pair counts per patch (hist[nb] = 0), then ctr[4]
-  uint32_t *ctr;     // [0] follow count, [1] overflow count, [2] rays traced
+  uint32_t *ctr;     // [0] follow count, [1] overflow count, [2] rays traced, [3] k_newton_lane chunks
   uint32_t *offs;    // [nb + 1] exclusive prefix of hist; offs[nb] = pair count
   uint32_t *cand;    // [kMaxCand][n]
   uint32_t *rank;    // [kMaxCand][n]
@@ -271,6 +284,7 @@ struct Work {
   float4 *pairs;     // [2][cap] pair records: (s.xyz, ray) and (d.xyz, patch) -- the ray travels with the pair
   uint32_t *fol;     // [cap] pair | what << 30
   uint32_t *ovf;     // [n]
+  uint32_t *lanes;   // [cap / 64 + 1] chunks for k_newton_lane (count in ctr[3])
   void *cub;
   size_t cub_bytes;
   uint32_t cap;      // kMaxCand * chunk
@@ -363,25 +377,29 @@ __global__ __launch_bounds__(kBlock) void k_traverse(MeshView m, const float *__
   }
   while (sp > 0) {
     const uint32_t node = __builtin_amdgcn_readfirstlane(stack[wv][--sp]);
-    // wave-uniform record read through the constant address space: scalar loads into SGPRs
-    const __attribute__((address_space(4))) bzr_host::Bvh4Node &nd =
-        *((const __attribute__((address_space(4))) bzr_host::Bvh4Node *)(uintptr_t)m.nodes + node);
+    // the whole 128-byte node in two 64-byte scalar loads and one wait (all words used unconditionally)
+    const cu32x16 *np = (const cu32x16 *)(uintptr_t)(m.nodes + node);
+    const u32x16 na = np[0], nb = np[1];
+    // words: lo.x[0..3] lo.y lo.z hi.x | hi.y hi.z child[0..3] pad
     bool hit[4];
 #pragma unroll
-    for (int c = 0; c < 4; ++c)
-      hit[c] = active && nd.child[c] != bzr_host::kEmptyChild &&
-               slab(make_float4(nd.lo[0][c], nd.lo[1][c], nd.lo[2][c], 0.0f),
-                    make_float4(nd.hi[0][c], nd.hi[1][c], nd.hi[2][c], 0.0f), s, inv);
+    for (int c = 0; c < 4; ++c) {
+      const float4 lo = make_float4(__uint_as_float(na[c]), __uint_as_float(na[4 + c]), __uint_as_float(na[8 + c]), 0.0f);
+      const float4 hi = make_float4(__uint_as_float(na[12 + c]), __uint_as_float(nb[c]), __uint_as_float(nb[4 + c]), 0.0f);
+      hit[c] = active & (nb[8 + c] != bzr_host::kEmptyChild) & slab(lo, hi, s, inv);
+    }
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       if (!__any(hit[c])) continue;
-      const uint32_t ch = nd.child[c];
+      const uint32_t ch = nb[8 + c];
       if (ch & bzr_host::kLeafFlag) {
-        const const_float *q = (const const_float *)(uintptr_t)m.leaf + 16u * (ch & ~bzr_host::kLeafFlag);
-        const float4 q0 = make_float4(q[0], q[1], q[2], q[3]), q1 = make_float4(q[4], q[5], q[6], q[7]);
-        const float4 q2 = make_float4(q[8], q[9], q[10], q[11]), q3 = make_float4(q[12], q[13], q[14], q[15]);
+        const u32x16 q = *((const cu32x16 *)(uintptr_t)m.leaf + (ch & ~bzr_host::kLeafFlag));
+        const float4 q0 = make_float4(__uint_as_float(q[0]), __uint_as_float(q[1]), __uint_as_float(q[2]), __uint_as_float(q[3]));
+        const float4 q1 = make_float4(__uint_as_float(q[4]), __uint_as_float(q[5]), __uint_as_float(q[6]), __uint_as_float(q[7]));
+        const float4 q2 = make_float4(__uint_as_float(q[8]), __uint_as_float(q[9]), __uint_as_float(q[10]), __uint_as_float(q[11]));
+        const float4 q3 = make_float4(__uint_as_float(q[12]), __uint_as_float(q[13]), __uint_as_float(q[14]), 0.0f);
         if (hit[c] && planar_gate(q0, q1, q2, q3, s, d)) {
-          if (cnt < kMaxCand) w.cand[(size_t)cnt * n + i] = __float_as_uint(q3.w);
+          if (cnt < kMaxCand) w.cand[(size_t)cnt * n + i] = q[15];
           cnt = cnt < kMaxCand ? cnt + 1 : kOverflow;
         }
       } else if (sp < kStack) {
@@ -405,27 +423,39 @@ __global__ __launch_bounds__(kBlock) void k_traverse(MeshView m, const float *__
   // lanes take their rank from the returned base.
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t listed = cnt <= kMaxCand ? cnt : 0u;
-  for (uint32_t j = 0; __any(j < listed); ++j) {
-    const bool pend = j < listed;
-    const uint32_t b = pend ? w.cand[(size_t)j * n + i] : 0u;
-    unsigned long long group = 0ull;
-    bool todo = pend;
-    for (;;) {
-      const unsigned long long mask = __ballot(todo);
-      if (mask == 0ull) break;
-      const uint32_t b0 = __builtin_amdgcn_readlane(b, __builtin_ctzll(mask));
-      const bool same = todo && b == b0;
-      const unsigned long long g = __ballot(same);
-      if (same) {
-        group = g;
-        todo = false;
+  // Four list slots per round: their candidate loads first, then the grouping, then all four rounds'
+  // returning atomics in flight together (one wait instead of four: vmcnt retires in issue order).
+  constexpr int kRankBatch = 4;
+  for (uint32_t j0 = 0; __any(j0 < listed); j0 += kRankBatch) {
+    uint32_t b[kRankBatch], leader[kRankBatch], below[kRankBatch], base[kRankBatch];
+#pragma unroll
+    for (int k = 0; k < kRankBatch; ++k) b[k] = j0 + k < listed ? w.cand[(size_t)(j0 + k) * n + i] : 0u;
+#pragma unroll
+    for (int k = 0; k < kRankBatch; ++k) {
+      const bool pend = j0 + k < listed;
+      unsigned long long group = 0ull;
+      bool todo = pend;
+      for (;;) {
+        const unsigned long long mask = __ballot(todo);
+        if (mask == 0ull) break;
+        const uint32_t b0 = __builtin_amdgcn_readlane(b[k], __builtin_ctzll(mask));
+        const bool same = todo && b[k] == b0;
+        const unsigned long long g = __ballot(same);
+        if (same) {
+          group = g;
+          todo = false;
+        }
       }
+      leader[k] = pend ? (uint32_t)__builtin_ctzll(group) : lane;
+      below[k] = lanes_below(group);
+      base[k] = 0u;
+      if (pend && lane == leader[k]) base[k] = atomicAdd(&w.hist[b[k]], (uint32_t)__popcll(group));
     }
-    const uint32_t leader = pend ? (uint32_t)__builtin_ctzll(group) : lane;
-    uint32_t base = 0;
-    if (pend && lane == leader) base = atomicAdd(&w.hist[b], (uint32_t)__popcll(group));
-    base = __shfl(base, (int)leader, 64);
-    if (pend) w.rank[(size_t)j * n + i] = base + lanes_below(group);
+#pragma unroll
+    for (int k = 0; k < kRankBatch; ++k) {
+      const uint32_t bs = __shfl(base[k], (int)leader[k], 64);
+      if (j0 + k < listed) w.rank[(size_t)(j0 + k) * n + i] = bs + below[k];
+    }
   }
 }
 
@@ -464,7 +494,8 @@ __device__ __forceinline__ void flush_follow(uint32_t *buf, uint32_t &nf, uint32
 __global__ __launch_bounds__(kBlock) void k_newton(const float *__restrict__ full, const uint32_t *__restrict__ total,
                                                    const float4 *__restrict__ pairs, float *__restrict__ slot,
                                                    uint32_t cap, unsigned long long *__restrict__ key,
-                                                   uint32_t *__restrict__ fol, uint32_t *__restrict__ nfol) {
+                                                   uint32_t *__restrict__ fol, uint32_t *__restrict__ nfol,
+                                                   uint32_t *__restrict__ lanes, uint32_t *__restrict__ nlanes) {
   __shared__ uint32_t fbuf[kWaves][kFolBuf];
   const uint32_t wv = threadIdx.x >> 6;
   uint32_t nf = 0;  // staged follow requests of this wave (uniform)
@@ -490,6 +521,13 @@ __global__ __launch_bounds__(kBlock) void k_newton(const float *__restrict__ ful
     }
     bool is_fol = false;
     uint32_t fol_entry = 0;
+    // a chunk spanning many small buckets would take one pass per patch here: hand it to k_newton_lane
+    const uint32_t bprev = __shfl_up(b, 1u, 64);
+    const uint32_t distinct = (uint32_t)__popcll(__ballot(todo && (lane == 0u || b != bprev)));
+    if (distinct > kLaneThreshold) {
+      if (lane == 0u) lanes[atomicAdd(nlanes, 1u)] = q;
+      todo = false;
+    }
     for (;;) {
       const unsigned long long mask = __ballot(todo);
       if (mask == 0ull) break;
@@ -499,7 +537,8 @@ __global__ __launch_bounds__(kBlock) void k_newton(const float *__restrict__ ful
       const auto pa = uniform_patch(full, b0);
       if (todo && b == b0) {
         todo = false;
-        const Hit h = patch_intersect(pa, s, d, false);
+        // every pair passed this patch's planar gate in k_traverse (same arithmetic, same record values)
+        const Hit h = patch_intersect<BZR_NEWTON_GATED != 0>(pa, s, d, false);
         if (h.what == kIntersect) record(slot, cap, p, h, b0, &key[ray]);
         is_fol = h.what <= kFollow2;
         fol_entry = p | (h.what << 30);
@@ -514,6 +553,40 @@ __global__ __launch_bounds__(kBlock) void k_newton(const float *__restrict__ ful
     }
   }
   if (nf) flush_follow(fbuf[wv], nf, fol, nfol, lane);
+}
+
+// The chunks k_newton handed over (more than kLaneThreshold distinct patches): every lane runs its own
+// pair with its own patch record in VGPRs, so a fragmented chunk costs one pass instead of one per patch.
+__global__ __launch_bounds__(kBlock) void k_newton_lane(const float *__restrict__ full, const uint32_t *__restrict__ total,
+                                                        const float4 *__restrict__ pairs, float *__restrict__ slot,
+                                                        uint32_t cap, unsigned long long *__restrict__ key,
+                                                        uint32_t *__restrict__ fol, uint32_t *__restrict__ nfol,
+                                                        const uint32_t *__restrict__ lanes,
+                                                        const uint32_t *__restrict__ nlanes) {
+  const uint32_t P = __builtin_amdgcn_readfirstlane(*total);
+  const uint32_t C = __builtin_amdgcn_readfirstlane(*nlanes);
+  const uint32_t lane = threadIdx.x & 63u;
+  for (uint32_t c = blockIdx.x * kWaves + (threadIdx.x >> 6); c < C; c += gridDim.x * kWaves) {
+    const uint32_t p = lanes[c] * 64u + lane;
+    bool is_fol = false;
+    uint32_t fol_entry = 0;
+    if (p < P) {
+      const float4 a = pairs[p], e = pairs[(size_t)cap + p];
+      const uint32_t b = __float_as_uint(e.w);
+      const Patch pa = load_patch(full + (size_t)rec::kWords * b);
+      const Hit h = patch_intersect<BZR_NEWTON_GATED != 0>(pa, mk(a.x, a.y, a.z), mk(e.x, e.y, e.z), false);
+      if (h.what == kIntersect) record(slot, cap, p, h, b, &key[__float_as_uint(a.w)]);
+      is_fol = h.what <= kFollow2;
+      fol_entry = p | (h.what << 30);
+    }
+    const unsigned long long fm = __ballot(is_fol);
+    if (fm) {
+      uint32_t base = 0;
+      if (lane == 0u) base = atomicAdd(nfol, (uint32_t)__popcll(fm));
+      base = __builtin_amdgcn_readfirstlane(base);
+      if (is_fol) fol[base + lanes_below(fm)] = fol_entry;
+    }
+  }
 }
 
 __global__ __launch_bounds__(kBlock) void k_follow(MeshView m, const float *__restrict__ rays, uint32_t ld,
@@ -614,6 +687,7 @@ __global__ void k_count(Work w, uint32_t nb, unsigned long long *__restrict__ co
   counters[BZR_COUNTER_PAIRS] += w.offs[nb];
   counters[BZR_COUNTER_FOLLOWS] += w.ctr[0];
   counters[BZR_COUNTER_OVERFLOW_RAYS] += w.ctr[1];
+  counters[BZR_COUNTER_LANE_CHUNKS] += w.ctr[3];
 }
 
 __global__ void k_fill(uint32_t *__restrict__ a, uint32_t value, uint32_t n) {
@@ -813,17 +887,19 @@ uint32_t resident_blocks(bzr_ctx *ctx, K kernel) {
 // Workspace of the culled path for chunks of up to `chunk` rays over meshes of up to `nb` patches.
 bzr_status ensure_work(bzr_ctx *ctx, uint32_t chunk, uint32_t nb, Work &w) {
   size_t cub_bytes = 0;
+  const uint32_t hn = nb;  // histogram slots, one per patch
   BZR_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, cub_bytes, static_cast<uint32_t *>(nullptr),
-                                           static_cast<uint32_t *>(nullptr), nb + 1, ctx->stream));
+                                           static_cast<uint32_t *>(nullptr), hn + 1, ctx->stream));
   const size_t cap = (size_t)kMaxCand * chunk;
-  const size_t bytes = round256((size_t)(nb + 5) * 4) + round256((size_t)(nb + 1) * 4) + 2 * round256(cap * 4) +
+  const size_t bytes = round256((size_t)(hn + 5) * 4) + round256((size_t)(hn + 1) * 4) + 2 * round256(cap * 4) +
                        round256((size_t)chunk * 4) + round256((size_t)chunk * 8) + round256(kSlotWords * cap * 4) +
-                       round256(cap * 32) + round256(cap * 4) + round256((size_t)chunk * 4) + round256(cub_bytes);
+                       round256(cap * 32) + round256(cap * 4) + round256((size_t)chunk * 4) + round256((cap / 64 + 1) * 4) +
+                       round256(cub_bytes);
   if (bzr_status s = ensure_buffer(ctx->work, ctx->work_bytes, bytes)) return s;
   Staging st{static_cast<char *>(ctx->work)};
-  w.hist = st.take<uint32_t>(nb + 5);
-  w.ctr = w.hist + nb + 1;
-  w.offs = st.take<uint32_t>(nb + 1);
+  w.hist = st.take<uint32_t>(hn + 5);
+  w.ctr = w.hist + hn + 1;
+  w.offs = st.take<uint32_t>(hn + 1);
   w.cand = st.take<uint32_t>(cap);
   w.rank = st.take<uint32_t>(cap);
   w.count = st.take<uint32_t>(chunk);
@@ -832,6 +908,7 @@ bzr_status ensure_work(bzr_ctx *ctx, uint32_t chunk, uint32_t nb, Work &w) {
   w.pairs = st.take<float4>(2 * cap);
   w.fol = st.take<uint32_t>(cap);
   w.ovf = st.take<uint32_t>(chunk);
+  w.lanes = st.take<uint32_t>(cap / 64 + 1);
   w.cub = st.take<char>(cub_bytes ? cub_bytes : 1);
   w.cub_bytes = cub_bytes;
   w.cap = static_cast<uint32_t>(cap);
@@ -847,19 +924,22 @@ template <int kMode>
 bzr_status run_culled(bzr_ctx *ctx, const MeshView &mv, const float *rays, uint32_t ld, uint32_t off, uint32_t n,
                       const uint32_t *alive, const Out &o, Work &w) {
   const uint32_t nb = mv.n;
-  BZR_HIP(hipMemsetAsync(w.hist, 0, (size_t)(nb + 5) * 4, ctx->stream));
+  const uint32_t hn = nb;
+  BZR_HIP(hipMemsetAsync(w.hist, 0, (size_t)(hn + 5) * 4, ctx->stream));
   launch(ctx, BZR_KERNEL_TRAVERSE, k_traverse, dim3(grid_for(n)), mv, rays, ld, off, alive, n, w,
          uint32_t(ctx->counting ? 1u : 0u));
   {
     Span sp(ctx, BZR_KERNEL_BUCKET);
-    BZR_HIP(hipcub::DeviceScan::ExclusiveSum(w.cub, w.cub_bytes, w.hist, w.offs, nb + 1, ctx->stream));
+    BZR_HIP(hipcub::DeviceScan::ExclusiveSum(w.cub, w.cub_bytes, w.hist, w.offs, hn + 1, ctx->stream));
     launch(ctx, -1, k_scatter, dim3(grid_for(n)), rays, ld, off, n, w);
   }
   // persistent grid: the resident capacity of the device, never more than the worst-case chunk count
   const uint32_t gn = std::min<uint32_t>(std::max<uint32_t>((kMaxCand * n + kBlock - 1) / kBlock, 1u),
                                          resident_blocks(ctx, k_newton));
-  launch(ctx, BZR_KERNEL_NEWTON, k_newton, dim3(gn), mv.full, w.offs + nb, w.pairs, w.slot, w.cap, w.key, w.fol,
-         w.ctr);
+  launch(ctx, BZR_KERNEL_NEWTON, k_newton, dim3(gn), mv.full, w.offs + hn, w.pairs, w.slot, w.cap, w.key, w.fol,
+         w.ctr, w.lanes, w.ctr + 3);
+  launch(ctx, BZR_KERNEL_NEWTON_LANE, k_newton_lane, dim3(std::min<uint32_t>(std::max<uint32_t>(n / 1024u, 1u), 1024u)),
+         mv.full, w.offs + hn, w.pairs, w.slot, w.cap, w.key, w.fol, w.ctr, w.lanes, w.ctr + 3);
   launch(ctx, BZR_KERNEL_FOLLOW, k_follow, dim3(std::min<uint32_t>(grid_for(n / 8 + 1), 1024u)), mv, rays, ld, off,
          w);
   launch(ctx, BZR_KERNEL_FINISH, k_finish<kMode>, dim3(grid_for(n)), rays, ld, off, n, w, o);

@@ -115,7 +115,8 @@ enum {
   BZR_KERNEL_REFRACT_SCAN = 7,
   BZR_KERNEL_CHAIN_SCAN = 8,
   BZR_KERNEL_PATCH = 9,
-  BZR_KERNEL_COUNT = 10
+  BZR_KERNEL_NEWTON_LANE = 10,    /* Newton stage for fragmented pair chunks, one patch record per lane */
+  BZR_KERNEL_COUNT = 11
 };
 /* While enabled, every launch is bracketed by hipEvents on the context's stream. */
 bzr_status bzr_ctx_timing(bzr_ctx *ctx, int32_t enable);
@@ -129,7 +130,8 @@ enum {
   BZR_COUNTER_PAIRS = 1,         /* (ray, patch) pairs that passed the planar gate: Newton runs */
   BZR_COUNTER_FOLLOWS = 2,       /* follow-side retries on a neighbour patch: Newton runs */
   BZR_COUNTER_OVERFLOW_RAYS = 3, /* rays resolved by the in-order full scan */
-  BZR_COUNTER_COUNT = 4
+  BZR_COUNTER_LANE_CHUNKS = 4,   /* 64-pair chunks spanning many patches, run one record per lane */
+  BZR_COUNTER_COUNT = 5
 };
 /* While enabled, each culled segment adds its counts on the device (one tiny kernel per segment). */
 bzr_status bzr_ctx_counters(bzr_ctx *ctx, int32_t enable);
