@@ -101,6 +101,22 @@ constexpr int kStack = 64;
 typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
 typedef __attribute__((address_space(4))) const u32x16 cu32x16;
 
+// Blocks are dealt round-robin to the 8 XCDs (each with its own L2 and scalar caches).  This maps
+// block b to a bijective index under which each XCD owns one contiguous range of the grid, so the
+// blocks an XCD runs together work on neighbouring rays (same BVH nodes, same patches).
+constexpr uint32_t kXcds = 8;
+__device__ __forceinline__ uint32_t xcd_contiguous(uint32_t b, uint32_t nblocks) {
+  const uint32_t q = nblocks / kXcds, r = nblocks % kXcds, x = b % kXcds;
+  return x * q + (x < r ? x : r) + b / kXcds;
+}
+// BZR_NEWTON_XCD (default 1): k_newton waves take chunks in XCD-contiguous order (scalar-cache reuse).
+#ifndef BZR_NEWTON_XCD
+#define BZR_NEWTON_XCD 0
+#endif
+// Blocks of k_overflow (one overflow ray per block at a time, grid-stride over the list).
+#ifndef BZR_OVERFLOW_BLOCKS
+#define BZR_OVERFLOW_BLOCKS 256u
+#endif
 // BZR_NEWTON_GATED (default 1): k_newton skips the planar gate its pairs already passed in k_traverse.
 #ifndef BZR_NEWTON_GATED
 #define BZR_NEWTON_GATED 1
@@ -280,7 +296,7 @@ struct Work {
   uint32_t *rank;    // [kMaxCand][n]
   uint32_t *count;   // [n]
   unsigned long long *key;  // [n]
-  float *slot;       // [kSlotWords][cap] per-pair hit
+  float *slot;       // [cap][kSlotWords] per-pair hit (AoS, 48 bytes)
   float4 *pairs;     // [2][cap] pair records: (s.xyz, ray) and (d.xyz, patch) -- the ray travels with the pair
   uint32_t *fol;     // [cap] pair | what << 30
   uint32_t *ovf;     // [n]
@@ -337,29 +353,20 @@ __device__ __forceinline__ uint32_t lanes_below(unsigned long long mask) {
 // beat the reference's initial FLT_MAX (NaN, FLT_MAX, +inf) is dropped; -0 ties with +0.
 __device__ __forceinline__ void record(float *__restrict__ slot, uint32_t cap, uint32_t p, const Hit &h, uint32_t src,
                                        unsigned long long *key) {
+  (void)cap;
   if (!(h.t < FLT_MAX)) return;
-  slot[p] = h.t;
-  slot[(size_t)1 * cap + p] = h.point.x;
-  slot[(size_t)2 * cap + p] = h.point.y;
-  slot[(size_t)3 * cap + p] = h.point.z;
-  slot[(size_t)4 * cap + p] = h.cs;
-  slot[(size_t)5 * cap + p] = h.bary.x;
-  slot[(size_t)6 * cap + p] = h.bary.y;
-  slot[(size_t)7 * cap + p] = h.bary.z;
-  slot[(size_t)8 * cap + p] = h.normal.x;
-  slot[(size_t)9 * cap + p] = h.normal.y;
-  slot[(size_t)10 * cap + p] = h.normal.z;
-  slot[(size_t)11 * cap + p] = __uint_as_float(src);
+  float4 *r = reinterpret_cast<float4 *>(slot) + (size_t)3 * p;  // AoS: 48 bytes per pair
+  r[0] = make_float4(h.t, h.point.x, h.point.y, h.point.z);
+  r[1] = make_float4(h.cs, h.bary.x, h.bary.y, h.bary.z);
+  r[2] = make_float4(h.normal.x, h.normal.y, h.normal.z, __uint_as_float(src));
   atomicMin(key, ((unsigned long long)t_order(h.t) << 32) | p);
 }
 
 // Candidate search.  `alive` (optional): a ray is traced iff alive[off + i] != BZR_RR_NONE.
-__global__ __launch_bounds__(kBlock) void k_traverse(MeshView m, const float *__restrict__ rays, uint32_t ld,
-                                                     uint32_t off, const uint32_t *__restrict__ alive, uint32_t n,
-                                                     Work w, uint32_t count_rays) {
-  __shared__ uint32_t stack[kWaves][kStack];
-  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  const uint32_t wv = threadIdx.x >> 6;
+// One wave's 64 rays i (lane l of the wave holds ray i); `stk` is the wave's LDS stack.
+__device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__restrict__ rays, uint32_t ld,
+                                              uint32_t off, const uint32_t *__restrict__ alive, uint32_t n,
+                                              const Work &w, uint32_t count_rays, uint32_t i, uint32_t *stk) {
   bool active = i < n && (alive == nullptr || alive[off + i] != BZR_RR_NONE);
   f3 s = mk(0.0f, 0.0f, 0.0f), d = s;
   if (i < n) load_ray(rays, ld, off + i, s, d);
@@ -372,38 +379,39 @@ __global__ __launch_bounds__(kBlock) void k_traverse(MeshView m, const float *__
   f3 inv = mk(safe_inv(d.x), safe_inv(d.y), safe_inv(d.z));
   int sp = 0;
   if (m.n > 0 && __any(active)) {
-    stack[wv][0] = 0u;
+    stk[0] = 0u;
     sp = 1;
   }
   while (sp > 0) {
-    const uint32_t node = __builtin_amdgcn_readfirstlane(stack[wv][--sp]);
+    const uint32_t node = __builtin_amdgcn_readfirstlane(stk[--sp]);
     // the whole 128-byte node in two 64-byte scalar loads and one wait (all words used unconditionally)
     const cu32x16 *np = (const cu32x16 *)(uintptr_t)(m.nodes + node);
     const u32x16 na = np[0], nb = np[1];
     // words: lo.x[0..3] lo.y lo.z hi.x | hi.y hi.z child[0..3] pad
     bool hit[4];
+    uint32_t ch[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       const float4 lo = make_float4(__uint_as_float(na[c]), __uint_as_float(na[4 + c]), __uint_as_float(na[8 + c]), 0.0f);
       const float4 hi = make_float4(__uint_as_float(na[12 + c]), __uint_as_float(nb[c]), __uint_as_float(nb[4 + c]), 0.0f);
-      hit[c] = active & (nb[8 + c] != bzr_host::kEmptyChild) & slab(lo, hi, s, inv);
+      ch[c] = nb[8 + c];
+      hit[c] = active & (ch[c] != bzr_host::kEmptyChild) & slab(lo, hi, s, inv);
     }
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       if (!__any(hit[c])) continue;
-      const uint32_t ch = nb[8 + c];
-      if (ch & bzr_host::kLeafFlag) {
-        const u32x16 q = *((const cu32x16 *)(uintptr_t)m.leaf + (ch & ~bzr_host::kLeafFlag));
-        const float4 q0 = make_float4(__uint_as_float(q[0]), __uint_as_float(q[1]), __uint_as_float(q[2]), __uint_as_float(q[3]));
-        const float4 q1 = make_float4(__uint_as_float(q[4]), __uint_as_float(q[5]), __uint_as_float(q[6]), __uint_as_float(q[7]));
-        const float4 q2 = make_float4(__uint_as_float(q[8]), __uint_as_float(q[9]), __uint_as_float(q[10]), __uint_as_float(q[11]));
-        const float4 q3 = make_float4(__uint_as_float(q[12]), __uint_as_float(q[13]), __uint_as_float(q[14]), 0.0f);
+      if (ch[c] & bzr_host::kLeafFlag) {
+        const u32x16 r = *((const cu32x16 *)(uintptr_t)m.leaf + (ch[c] & ~bzr_host::kLeafFlag));
+        const float4 q0 = make_float4(__uint_as_float(r[0]), __uint_as_float(r[1]), __uint_as_float(r[2]), __uint_as_float(r[3]));
+        const float4 q1 = make_float4(__uint_as_float(r[4]), __uint_as_float(r[5]), __uint_as_float(r[6]), __uint_as_float(r[7]));
+        const float4 q2 = make_float4(__uint_as_float(r[8]), __uint_as_float(r[9]), __uint_as_float(r[10]), __uint_as_float(r[11]));
+        const float4 q3 = make_float4(__uint_as_float(r[12]), __uint_as_float(r[13]), __uint_as_float(r[14]), 0.0f);
         if (hit[c] && planar_gate(q0, q1, q2, q3, s, d)) {
-          if (cnt < kMaxCand) w.cand[(size_t)cnt * n + i] = q[15];
+          if (cnt < kMaxCand) w.cand[(size_t)cnt * n + i] = r[15];
           cnt = cnt < kMaxCand ? cnt + 1 : kOverflow;
         }
       } else if (sp < kStack) {
-        stack[wv][sp++] = ch;
+        stk[sp++] = ch[c];
       } else {  // traversal stack exhausted: resolve these rays with the full scan
         if (hit[c]) cnt = kOverflow;
       }
@@ -459,6 +467,16 @@ __global__ __launch_bounds__(kBlock) void k_traverse(MeshView m, const float *__
   }
 }
 
+// Candidate search, one 64-ray wave per 64 consecutive rays.
+__global__ __launch_bounds__(kBlock) void k_traverse(MeshView m, const float *__restrict__ rays, uint32_t ld,
+                                                     uint32_t off, const uint32_t *__restrict__ alive, uint32_t n,
+                                                     Work w, uint32_t count_rays) {
+  __shared__ uint32_t stack[kWaves][kStack];
+  const uint32_t b = xcd_contiguous(blockIdx.x, gridDim.x);
+  traverse_rays(m, rays, ld, off, alive, n, w, count_rays, b * kBlock + threadIdx.x, stack[threadIdx.x >> 6]);
+}
+
+
 __global__ __launch_bounds__(kBlock) void k_scatter(const float *__restrict__ rays, uint32_t ld, uint32_t off,
                                                     uint32_t n, Work w) {
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
@@ -503,7 +521,11 @@ __global__ __launch_bounds__(kBlock) void k_newton(const float *__restrict__ ful
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t nchunks = (P + 63u) / 64u;
   const uint32_t W = gridDim.x * kWaves;
+#if BZR_NEWTON_XCD
+  uint32_t q = xcd_contiguous(blockIdx.x, gridDim.x) * kWaves + (threadIdx.x >> 6);
+#else
   uint32_t q = blockIdx.x * kWaves + (threadIdx.x >> 6);
+#endif
   float4 a = make_float4(0.0f, 0.0f, 0.0f, 0.0f), e = a;
   if (q < nchunks && q * 64u + lane < P) {
     a = pairs[q * 64u + lane];
@@ -618,14 +640,16 @@ __global__ __launch_bounds__(kBlock) void k_finish(const float *rays, uint32_t l
   const unsigned long long k = w.key[i];
   if (k != ~0ull) {
     const uint32_t p = static_cast<uint32_t>(k);
-    const size_t c = w.cap;
-    h.t = w.slot[p];
-    h.point = mk(w.slot[c + p], w.slot[2 * c + p], w.slot[3 * c + p]);
-    h.cs = w.slot[4 * c + p];
-    h.bary = mk(w.slot[5 * c + p], w.slot[6 * c + p], w.slot[7 * c + p]);
-    h.normal = mk(w.slot[8 * c + p], w.slot[9 * c + p], w.slot[10 * c + p]);
+
+    const float4 *r = reinterpret_cast<const float4 *>(w.slot) + (size_t)3 * p;  // AoS: 48 bytes per pair
+    const float4 r0 = r[0], r1 = r[1], r2 = r[2];
+    h.t = r0.x;
+    h.point = mk(r0.y, r0.z, r0.w);
+    h.cs = r1.x;
+    h.bary = mk(r1.y, r1.z, r1.w);
+    h.normal = mk(r2.x, r2.y, r2.z);
     h.what = kIntersect;
-    patch = __float_as_uint(w.slot[11 * c + p]);
+    patch = __float_as_uint(r2.w);
   }
   emit<kMode>(o, ld, gi, s, d, h, patch);
 }
@@ -833,21 +857,27 @@ hipEvent_t take_event(bzr_ctx *ctx) {
   return e;
 }
 
-// Launch on the context's stream; with timing enabled, bracket the launch with events.
+// Launch on `stream`; with timing enabled, bracket the launch with events on that stream.
 template <typename... Args>
-void launch(bzr_ctx *ctx, int kernel_id, void (*kernel)(Args...), dim3 grid, typename std::decay<Args>::type... args) {
+void launch_on(bzr_ctx *ctx, hipStream_t stream, int kernel_id, void (*kernel)(Args...), dim3 grid,
+               typename std::decay<Args>::type... args) {
   const bool timed = ctx->timing && kernel_id >= 0;
   hipEvent_t a = nullptr, b = nullptr;
   if (timed) {
     a = take_event(ctx);
     b = take_event(ctx);
-    (void)hipEventRecord(a, ctx->stream);
+    (void)hipEventRecord(a, stream);
   }
-  hipLaunchKernelGGL(kernel, grid, dim3(kBlock), 0, ctx->stream, args...);
+  hipLaunchKernelGGL(kernel, grid, dim3(kBlock), 0, stream, args...);
   if (timed) {
-    (void)hipEventRecord(b, ctx->stream);
+    (void)hipEventRecord(b, stream);
     ctx->marks.push_back({kernel_id, a, b});
   }
+}
+// Launch on the context's stream.
+template <typename... Args>
+void launch(bzr_ctx *ctx, int kernel_id, void (*kernel)(Args...), dim3 grid, typename std::decay<Args>::type... args) {
+  launch_on(ctx, ctx->stream, kernel_id, kernel, grid, args...);
 }
 
 // Event bracket around a group of launches (timing enabled only).
@@ -943,7 +973,8 @@ bzr_status run_culled(bzr_ctx *ctx, const MeshView &mv, const float *rays, uint3
   launch(ctx, BZR_KERNEL_FOLLOW, k_follow, dim3(std::min<uint32_t>(grid_for(n / 8 + 1), 1024u)), mv, rays, ld, off,
          w);
   launch(ctx, BZR_KERNEL_FINISH, k_finish<kMode>, dim3(grid_for(n)), rays, ld, off, n, w, o);
-  launch(ctx, BZR_KERNEL_OVERFLOW, k_overflow<kMode>, dim3(std::min<uint32_t>(n, 2048u)), mv, rays, ld, off, w, o);
+  launch(ctx, BZR_KERNEL_OVERFLOW, k_overflow<kMode>, dim3(std::min<uint32_t>(n, BZR_OVERFLOW_BLOCKS)), mv, rays, ld, off,
+         w, o);
   if (ctx->counting && ctx->counters)
     hipLaunchKernelGGL(k_count, dim3(1), dim3(64), 0, ctx->stream, w, nb, ctx->counters);
   BZR_HIP(hipGetLastError());
@@ -975,8 +1006,9 @@ extern "C" bzr_status bzr_ctx_create(int32_t device, bzr_ctx **out) {
   c->device = device;
   hipError_t e = hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking);
   if (e != hipSuccess) {
+    if (c->own) (void)hipStreamDestroy(c->own);
     delete c;
-    return set_error(BZR_ERR_HIP, std::string("hipStreamCreate: ") + hipGetErrorString(e));
+    return set_error(BZR_ERR_HIP, std::string("context streams: ") + hipGetErrorString(e));
   }
   c->stream = c->own;
   *out = c;
