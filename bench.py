@@ -10,8 +10,9 @@ the two-lens 4096x4096 chain instead.
 A step = one frame: the whole chain over this rank's primary rays, inputs already resident in HBM,
 results bit-identical to the reference restatement (tests/test_gpu_parity.py).  N GPUs = N processes
 (torch.distributed over RCCL): weak scaling -- the image grows to side x (side*N) pixels, 64x64
-tiles dealt round-robin, side^2 rays per rank, and each frame's results are gathered to rank 0 over
-RCCL inside the timed step (--gather step, the default).
+tiles dealt round-robin, side^2 rays per rank, and each frame's results (28 B per primary) are gathered to
+rank 0 over RCCL inside the timed region (--gather step, the default), double-buffered so frame k's
+gather overlaps frame k+1's tracing.
 
 Prints ONE JSON line on rank 0; fields are described in DESIGN.md (Measurement).
 """
@@ -89,10 +90,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # BZR_BENCH_DEVICE: pin every rank to one device index (multi-rank rehearsal on a 1-GPU box only)
+    local = int(os.environ.get("BZR_BENCH_DEVICE", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("BZR_BENCH_BACKEND", "nccl")  # "gloo": rehearsal on a 1-GPU box only
+        dist.init_process_group(backend, device_id=dev if backend == "nccl" else None)
 
     cfg = CONFIGS[a.config]
     side = a.side or cfg.side
@@ -117,8 +121,13 @@ def main():
     out_rays = torch.empty((6, n), dtype=torch.float32, device=dev)
     out_status = torch.empty(n, dtype=torch.int32, device=dev)
     out_seg = torch.empty(n, dtype=torch.int32, device=dev)
-    packed = torch.empty((frame.PACKED_ROWS, n), dtype=torch.float32, device=dev)
-    gather_list = [torch.empty_like(packed) for _ in range(world)] if (world > 1 and rank == 0) else None
+    # double-buffered frame gather: frame k's packed results travel to rank 0 (RCCL, its own stream)
+    # while frame k+1 is traced; a buffer is refilled only after its previous gather completed
+    packed = [torch.empty((frame.PACKED_ROWS, n), dtype=torch.float32, device=dev) for _ in range(2)]
+    gather_lists = [[torch.empty_like(packed[0]) for _ in range(world)] if (world > 1 and rank == 0) else None
+                    for _ in range(2)]
+    pending = [None, None]
+    frames = [0]
 
     def step(ev=None):
         if ev is not None:
@@ -127,16 +136,28 @@ def main():
         if ev is not None:
             ev[1].record(stream)
         if world > 1 and a.gather == "step":
-            frame.pack(out_rays, out_status, out_seg, packed)
-            frame.gather(packed, world, rank, gather_list=gather_list)
+            slot = frames[0] % 2
+            if pending[slot] is not None:
+                pending[slot].wait()
+            frame.pack(out_rays, out_status, out_seg, packed[slot])
+            pending[slot] = frame.gather(packed[slot], world, rank, gather_list=gather_lists[slot], async_op=True)
+        frames[0] += 1
+
+    def drain():
+        for k in range(2):
+            if pending[k] is not None:
+                pending[k].wait()
+                pending[k] = None
 
     for _ in range(a.warmup):
         step()
+    drain()
     torch.cuda.synchronize()
     # work counters of one frame (device-side; measured here, outside the timed region)
     ctx.counters(True)
     ctx.counters_report()
     step()
+    drain()
     work_cnt = ctx.counters_report()
     ctx.counters(False)
     seg_local = int(out_seg.sum().item())
@@ -152,6 +173,7 @@ def main():
     t_start = time.perf_counter()
     for k in range(a.steps):
         step(events[k])
+    drain()  # the last frames' gathers complete inside the timed region
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -163,6 +185,7 @@ def main():
     ctx.timing_report()  # reset
     for k in range(a.steps):
         step()
+    drain()
     kernels = ctx.timing_report()
     ctx.timing(False)
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -239,7 +262,7 @@ def main():
                 "primaries_per_gpu": n,
                 "segments_per_step": seg_total,
                 "patches": n_patch,
-                "parallelism": f"image tiles x{world}" + (", RCCL gather to rank 0 in every step"
+                "parallelism": f"image tiles x{world}" + (", RCCL gather of every frame to rank 0 (overlapped with the next frame)"
                                                           if world > 1 and a.gather == "step" else ""),
                 "scan": "BVH-culled (bit-identical to brute force)" if a.accel == "bvh" else "brute force",
                 "numerics": "parity: bit-identical to the CPU oracle",

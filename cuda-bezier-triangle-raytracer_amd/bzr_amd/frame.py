@@ -4,7 +4,8 @@ One process per GPU (torch.distributed; "nccl" = RCCL over xGMI on MI355X, "gloo
 Rays are independent, so the only exchange is the final gather.  The image is
 `width` x `height` pixels; 64x64 tiles are dealt round-robin to ranks (configs.shard_pixels) so
 every rank gets a similar mix of lens-hitting and missing rays.  A rank's result for one frame is a
-packed [8, n] float32 tensor: the 6 ray rows, then status and segment counts as raw 32-bit words.
+packed [7, n] float32 tensor: the 6 ray rows, then one raw 32-bit word per ray holding the status
+(bits 0-7) and the segment count (bits 8-15): 28 bytes per primary ray cross xGMI.
 """
 from __future__ import annotations
 
@@ -12,7 +13,7 @@ import numpy as np
 
 from .configs import Config, rays_for, shard_pixels
 
-PACKED_ROWS = 8
+PACKED_ROWS = 7
 
 
 def rank_rays(cfg: Config, rank: int, world: int, width: int, height: int):
@@ -22,22 +23,25 @@ def rank_rays(cfg: Config, rank: int, world: int, width: int, height: int):
 
 
 def pack(out_rays, out_status, out_segments, packed):
-    """Write one frame's results into `packed` [8, n] (torch tensors, same device)."""
+    """Write one frame's results into `packed` [7, n] (torch tensors, same device)."""
     import torch
 
     packed[:6].copy_(out_rays)
-    packed[6].copy_(out_status.view(torch.float32))
-    packed[7].copy_(out_segments.view(torch.float32))
+    word = out_status.to(torch.int32) | (out_segments.to(torch.int32) << 8)
+    packed[6].copy_(word.view(torch.float32))
     return packed
 
 
-def gather(packed, world: int, rank: int, dst: int = 0, gather_list=None):
-    """Gather every rank's packed frame on `dst` (collective; all ranks call it)."""
+def gather(packed, world: int, rank: int, dst: int = 0, gather_list=None, async_op: bool = False):
+    """Gather every rank's packed frame on `dst` (collective; all ranks call it).  With async_op the
+    collective's work handle is returned instead: the caller waits on it before reusing `packed`."""
     import torch.distributed as dist
 
     if world == 1:
-        return [packed]
-    dist.gather(packed, gather_list if rank == dst else None, dst=dst)
+        return None if async_op else [packed]
+    work = dist.gather(packed, gather_list if rank == dst else None, dst=dst, async_op=async_op)
+    if async_op:
+        return work
     return gather_list if rank == dst else None
 
 
@@ -52,6 +56,7 @@ def assemble(parts, cfg: Config, world: int, width: int, height: int):
         rows, cols = shard_pixels(cfg, r, world, side=width, height=height)
         flat = rows * width + cols
         rays[:, flat] = p[:6]
-        status[flat] = p[6].view(np.uint32)
-        seg[flat] = p[7].view(np.uint32)
+        word = np.ascontiguousarray(p[6]).view(np.uint32)
+        status[flat] = word & 0xFF
+        seg[flat] = (word >> 8) & 0xFF
     return rays, status, seg

@@ -109,6 +109,11 @@ __device__ __forceinline__ uint32_t xcd_contiguous(uint32_t b, uint32_t nblocks)
   const uint32_t q = nblocks / kXcds, r = nblocks % kXcds, x = b % kXcds;
   return x * q + (x < r ? x : r) + b / kXcds;
 }
+// Threads per k_traverse block: its waves share one CU (scalar cache) and take neighbouring rays.
+#ifndef BZR_TRAV_BLOCK
+#define BZR_TRAV_BLOCK 256
+#endif
+constexpr int kTravBlock = BZR_TRAV_BLOCK;
 // BZR_NEWTON_XCD (default 1): k_newton waves take chunks in XCD-contiguous order (scalar-cache reuse).
 #ifndef BZR_NEWTON_XCD
 #define BZR_NEWTON_XCD 0
@@ -468,12 +473,12 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
 }
 
 // Candidate search, one 64-ray wave per 64 consecutive rays.
-__global__ __launch_bounds__(kBlock) void k_traverse(MeshView m, const float *__restrict__ rays, uint32_t ld,
-                                                     uint32_t off, const uint32_t *__restrict__ alive, uint32_t n,
-                                                     Work w, uint32_t count_rays) {
-  __shared__ uint32_t stack[kWaves][kStack];
+__global__ __launch_bounds__(kTravBlock) void k_traverse(MeshView m, const float *__restrict__ rays, uint32_t ld,
+                                                         uint32_t off, const uint32_t *__restrict__ alive, uint32_t n,
+                                                         Work w, uint32_t count_rays) {
+  __shared__ uint32_t stack[kTravBlock / 64][kStack];
   const uint32_t b = xcd_contiguous(blockIdx.x, gridDim.x);
-  traverse_rays(m, rays, ld, off, alive, n, w, count_rays, b * kBlock + threadIdx.x, stack[threadIdx.x >> 6]);
+  traverse_rays(m, rays, ld, off, alive, n, w, count_rays, b * kTravBlock + threadIdx.x, stack[threadIdx.x >> 6]);
 }
 
 
@@ -859,7 +864,7 @@ hipEvent_t take_event(bzr_ctx *ctx) {
 
 // Launch on `stream`; with timing enabled, bracket the launch with events on that stream.
 template <typename... Args>
-void launch_on(bzr_ctx *ctx, hipStream_t stream, int kernel_id, void (*kernel)(Args...), dim3 grid,
+void launch_on(bzr_ctx *ctx, hipStream_t stream, dim3 block, int kernel_id, void (*kernel)(Args...), dim3 grid,
                typename std::decay<Args>::type... args) {
   const bool timed = ctx->timing && kernel_id >= 0;
   hipEvent_t a = nullptr, b = nullptr;
@@ -868,7 +873,7 @@ void launch_on(bzr_ctx *ctx, hipStream_t stream, int kernel_id, void (*kernel)(A
     b = take_event(ctx);
     (void)hipEventRecord(a, stream);
   }
-  hipLaunchKernelGGL(kernel, grid, dim3(kBlock), 0, stream, args...);
+  hipLaunchKernelGGL(kernel, grid, block, 0, stream, args...);
   if (timed) {
     (void)hipEventRecord(b, stream);
     ctx->marks.push_back({kernel_id, a, b});
@@ -877,7 +882,7 @@ void launch_on(bzr_ctx *ctx, hipStream_t stream, int kernel_id, void (*kernel)(A
 // Launch on the context's stream.
 template <typename... Args>
 void launch(bzr_ctx *ctx, int kernel_id, void (*kernel)(Args...), dim3 grid, typename std::decay<Args>::type... args) {
-  launch_on(ctx, ctx->stream, kernel_id, kernel, grid, args...);
+  launch_on(ctx, ctx->stream, dim3(kBlock), kernel_id, kernel, grid, args...);
 }
 
 // Event bracket around a group of launches (timing enabled only).
@@ -956,8 +961,8 @@ bzr_status run_culled(bzr_ctx *ctx, const MeshView &mv, const float *rays, uint3
   const uint32_t nb = mv.n;
   const uint32_t hn = nb;
   BZR_HIP(hipMemsetAsync(w.hist, 0, (size_t)(hn + 5) * 4, ctx->stream));
-  launch(ctx, BZR_KERNEL_TRAVERSE, k_traverse, dim3(grid_for(n)), mv, rays, ld, off, alive, n, w,
-         uint32_t(ctx->counting ? 1u : 0u));
+  launch_on(ctx, ctx->stream, dim3(kTravBlock), BZR_KERNEL_TRAVERSE, k_traverse, dim3((n + kTravBlock - 1) / kTravBlock),
+            mv, rays, ld, off, alive, n, w, uint32_t(ctx->counting ? 1u : 0u));
   {
     Span sp(ctx, BZR_KERNEL_BUCKET);
     BZR_HIP(hipcub::DeviceScan::ExclusiveSum(w.cub, w.cub_bytes, w.hist, w.offs, hn + 1, ctx->stream));
