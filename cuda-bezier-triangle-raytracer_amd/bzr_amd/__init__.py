@@ -66,6 +66,7 @@ _SIGS = {
     "bzr_patch_intersect": [_P, _P, _P, _P, _P, _U32, _P, _U32],
     "bzr_refract": [_P, _P, _F, _P, _P, _U32, _U32, _P, _P, _U32],
     "bzr_trace_chain": [_P, _P, _P, _U32, _P, _U32, _P, _P, _P, _U32],
+    "bzr_mesh_interpolate": [_P, _P, _I32, _P, _U32],
     "bzr_trimesh_create": [ctypes.POINTER(_P)],
     "bzr_trimesh_destroy": [_P],
     "bzr_trimesh_copy": [_P, ctypes.POINTER(_P)],
@@ -319,6 +320,17 @@ def trace_chain(ctx: Context, lenses, ri, rays, out_rays=None, out_status=None, 
     return out_rays, out_status, out_segments
 
 
+def interpolate(ctx: Context, mesh: DeviceMesh, divisor: int, out=None):
+    """BezierMesh::interpolate(divisor) on the device -> triangles [divisor^2 * n_patches, 3, 3] float32
+    (reference order: sub-triangle outer, patch inner).  `out` may be a CUDA tensor (stays on the device)."""
+    count = int(divisor) * int(divisor) * mesh.n
+    if out is None:
+        out = np.empty((count, 3, 3), np.float32)
+    o = _Buf(out, np.float32, True)
+    _check(lib().bzr_mesh_interpolate(ctx.handle, mesh.handle, int(divisor), o.ptr, _residency(o)))
+    return out
+
+
 # ------------------------------------------------------------ host preprocessing
 class TriMesh:
     """The reference's Mesh (host C++ in libbzr): generators, welding, orientation, Bezier build."""
@@ -432,6 +444,6 @@ class TriMesh:
 
 
 __all__ = [
-    "BzrError", "Context", "DeviceMesh", "TriMesh", "intersect", "patch_intersect", "refract", "trace_chain",
+    "BzrError", "Context", "DeviceMesh", "TriMesh", "intersect", "patch_intersect", "refract", "trace_chain", "interpolate",
     "device_count", "lib", "exported_symbols", "LIB_PATH",
 ]

@@ -1388,3 +1388,56 @@ extern "C" bzr_status bzr_trace_chain(bzr_ctx *ctx, const bzr_mesh *const *lense
   }
   return BZR_OK;
 }
+
+// ------------------------------------------------------------ tessellation
+extern "C" uint32_t bzr_internal_unit_subtriangles(int32_t divisor, float *out);  // host (patch_build.cpp)
+
+namespace {
+// BezierMesh::interpolate (reference/bezierMesh.cpp:55-66): output triangle t = k * nb + b is
+// sub-triangle k of patch b; its three vertices are BezierTriangle::interpolate at the sub-triangle's
+// barycentric corners (reference/bezierTriangle.cpp:105-121, patch_math.hpp `interpolate`).
+__global__ __launch_bounds__(kBlock) void k_tessellate(const float *__restrict__ full, uint32_t nb,
+                                                       const float *__restrict__ bary, uint64_t total,
+                                                       float *__restrict__ out) {
+  const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (t >= total) return;
+  const uint32_t k = static_cast<uint32_t>(t / nb), b = static_cast<uint32_t>(t % nb);
+  const PatchView<const float *> p{full + (size_t)rec::kWords * b};
+  const float *bk = bary + (size_t)9 * k;
+#pragma unroll
+  for (int v = 0; v < 3; ++v) {
+    const f3 q = interpolate(p, mk(bk[3 * v], bk[3 * v + 1], bk[3 * v + 2]));
+    out[(size_t)9 * t + 3 * v] = q.x;
+    out[(size_t)9 * t + 3 * v + 1] = q.y;
+    out[(size_t)9 * t + 3 * v + 2] = q.z;
+  }
+}
+}  // namespace
+
+extern "C" bzr_status bzr_mesh_interpolate(bzr_ctx *ctx, const bzr_mesh *mesh, int32_t divisor, float *out_xyz,
+                                           uint32_t flags) {
+  if (bzr_status s = check_ctx_mesh(ctx, mesh)) return s;
+  if (divisor < 1 || divisor > 4096) return set_error(BZR_ERR_INVALID_ARGUMENT, "divisor must be 1..4096");
+  const uint32_t K = static_cast<uint32_t>(divisor) * static_cast<uint32_t>(divisor);
+  const uint64_t total = (uint64_t)K * mesh->n;
+  if (total == 0) return BZR_OK;
+  if (!out_xyz) return set_error(BZR_ERR_INVALID_ARGUMENT, "null buffer");
+  DeviceGuard g(ctx->device);
+  std::vector<float> bary((size_t)K * 9);
+  if (bzr_internal_unit_subtriangles(divisor, bary.data()) != K)
+    return set_error(BZR_ERR_INVALID_ARGUMENT, "sub-triangle count mismatch");
+  const bool host = !(flags & BZR_DEVICE_PTRS);
+  const size_t bb = round256(bary.size() * 4), ob = (size_t)total * 9 * 4;
+  if (bzr_status s = ensure_buffer(ctx->scratch, ctx->scratch_bytes, bb + (host ? round256(ob) : 0))) return s;
+  Staging st{static_cast<char *>(ctx->scratch)};
+  float *d_bary = st.take<float>(bary.size());
+  float *d_out = host ? st.take<float>((size_t)total * 9) : out_xyz;
+  BZR_HIP(hipMemcpyAsync(d_bary, bary.data(), bary.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+  hipLaunchKernelGGL(k_tessellate, dim3(static_cast<uint32_t>((total + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                     ctx->stream, mesh->full, mesh->n, d_bary, total, d_out);
+  BZR_HIP(hipGetLastError());
+  if (host) BZR_HIP(hipMemcpyAsync(out_xyz, d_out, ob, hipMemcpyDeviceToHost, ctx->stream));
+  // the staged sub-triangle table must outlive the kernel: this call is synchronous
+  BZR_HIP(hipStreamSynchronize(ctx->stream));
+  return BZR_OK;
+}

@@ -252,3 +252,16 @@ Mesh BezierMesh::splitThickBezierTriangles() const {  // reference/bezierMesh.cp
   }
   return out;
 }
+
+// The barycentric sub-triangles of BezierMesh::interpolate (util::divide of the unit triangle, in the
+// reference's order, reference/3dGeomUtil.h:99-122): divisor^2 triangles x 3 vertices x 3 floats
+// into `out`.  The device tessellation (bzr_mesh_interpolate) evaluates the patches at these.
+extern "C" uint32_t bzr_internal_unit_subtriangles(int32_t divisor, float *out) {
+  uint32_t k = 0;
+  util::divide(kUnitBary, divisor, [&](Triangle &&b) {
+    for (uint32_t v = 0; v < 3u; ++v)
+      for (int32_t c = 0; c < 3; ++c) out[(size_t)k * 9u + v * 3u + c] = b[v](c);
+    ++k;
+  });
+  return k;
+}

@@ -166,6 +166,12 @@ bzr_status bzr_refract(bzr_ctx *ctx, const bzr_mesh *mesh, float refractive_inde
 bzr_status bzr_trace_chain(bzr_ctx *ctx, const bzr_mesh *const *lenses, const float *refractive_index,
                            uint32_t nlens, const float *rays_soa, uint32_t n, float *out_rays_soa,
                            uint32_t *out_status, uint32_t *out_segments, uint32_t flags);
+/* BezierMesh::interpolate(divisor) on the device (reference/bezierMesh.cpp:55-66): the tessellated
+ * surface, divisor^2 sub-triangles of every patch, in the reference's order (sub-triangle outer,
+ * patch inner).  out_xyz: divisor^2 * n_patches triangles x 3 vertices x 3 floats.  divisor >= 1.
+ * Bit-identical to the host bzr_bezier_interpolate of the same patches. */
+bzr_status bzr_mesh_interpolate(bzr_ctx *ctx, const bzr_mesh *mesh, int32_t divisor, float *out_xyz,
+                                uint32_t flags);
 
 /* ---- host preprocessing (reference Mesh / BezierMesh construction) ---- */
 enum { BZR_ENVELOPE_ELLIPSOID = 0, BZR_ENVELOPE_TESTLENS = 1 };
