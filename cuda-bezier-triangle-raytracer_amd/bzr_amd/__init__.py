@@ -67,6 +67,9 @@ _SIGS = {
     "bzr_refract": [_P, _P, _F, _P, _P, _U32, _U32, _P, _P, _U32],
     "bzr_trace_chain": [_P, _P, _P, _U32, _P, _U32, _P, _P, _P, _U32],
     "bzr_mesh_interpolate": [_P, _P, _I32, _P, _U32],
+    "bzr_emit": [_P, _P, ctypes.c_uint64, _U32, _P, _P, _U32],
+    "bzr_illuminate": [_P, _P, _P, _U32, _P, ctypes.c_uint64, _P, _P, _P, _U32],
+    "bzr_mesh_bounding_sphere": [_P, _P],
     "bzr_trimesh_create": [ctypes.POINTER(_P)],
     "bzr_trimesh_destroy": [_P],
     "bzr_trimesh_copy": [_P, ctypes.POINTER(_P)],
@@ -331,6 +334,53 @@ def interpolate(ctx: Context, mesh: DeviceMesh, divisor: int, out=None):
     return out
 
 
+# ------------------------------------------------------------ illumination
+class Emitter(ctypes.Structure):
+    """bzr_emitter: rectangle origin + a*edge_u + b*edge_v, parts_u x parts_v parts, points_per_part
+    points per part, rays_per_point rays per point, hemisphere around +x numbered by `belts`."""
+    _fields_ = [("origin", _F * 3), ("edge_u", _F * 3), ("edge_v", _F * 3), ("parts_u", _U32), ("parts_v", _U32),
+                ("points_per_part", _U32), ("rays_per_point", _U32), ("belts", _U32), ("seed", ctypes.c_uint64)]
+
+
+class Target(ctypes.Structure):
+    """bzr_target: origin + a*axis_u + b*axis_v, a < size_u, b < size_v, bins_u x bins_v cells."""
+    _fields_ = [("origin", _F * 3), ("axis_u", _F * 3), ("axis_v", _F * 3), ("size_u", _F), ("size_v", _F),
+                ("bins_u", _U32), ("bins_v", _U32)]
+
+
+ILLUM_STATS = ("emitted", "culled", "exited", "landed")  # BZR_ILLUM_* ids
+
+
+def emit(ctx: Context, em: Emitter, first: int, n: int, rays=None, patch=None):
+    """Rays first .. first+n-1 of the emitter -> (rays [6, n], hemisphere patch index [n])."""
+    rays = np.empty((6, n), np.float32) if rays is None else rays
+    patch = np.empty(n, np.uint32) if patch is None else patch
+    r, p = _Buf(rays, np.float32, True), _Buf(patch, np.uint32, True)
+    _check(lib().bzr_emit(ctx.handle, ctypes.byref(em), int(first), int(n), r.ptr, p.ptr, _residency(r, p)))
+    return rays, patch
+
+
+def illuminate(ctx: Context, lenses, ri, em: Emitter, total_rays: int, target: Target, hist=None):
+    """Emitter -> bounding-sphere cull -> refraction chain -> target counts.  Returns (hist [bins_v, bins_u]
+    uint32, accumulated into `hist` if given, stats dict)."""
+    nl = len(lenses)
+    handles = (_P * nl)(*[m.handle for m in lenses])
+    ris = (_F * nl)(*[float(x) for x in ri])
+    hist = np.zeros((target.bins_v, target.bins_u), np.uint32) if hist is None else hist
+    h = _Buf(hist, np.uint32, True)
+    stats = (ctypes.c_uint64 * 4)()
+    _check(lib().bzr_illuminate(ctx.handle, handles, ris, nl, ctypes.byref(em), int(total_rays), ctypes.byref(target),
+                                h.ptr, stats, _residency(h)))
+    return hist, dict(zip(ILLUM_STATS, [int(x) for x in stats]))
+
+
+def bounding_sphere(mesh: DeviceMesh) -> np.ndarray:
+    """The lens's Ritter sphere over its gate-region boxes: [cx, cy, cz, r]."""
+    out = (_F * 4)()
+    _check(lib().bzr_mesh_bounding_sphere(mesh.handle, out))
+    return np.array(list(out), np.float32)
+
+
 # ------------------------------------------------------------ host preprocessing
 class TriMesh:
     """The reference's Mesh (host C++ in libbzr): generators, welding, orientation, Bezier build."""
@@ -445,5 +495,6 @@ class TriMesh:
 
 __all__ = [
     "BzrError", "Context", "DeviceMesh", "TriMesh", "intersect", "patch_intersect", "refract", "trace_chain", "interpolate",
+    "Emitter", "Target", "emit", "illuminate", "bounding_sphere",
     "device_count", "lib", "exported_symbols", "LIB_PATH",
 ]

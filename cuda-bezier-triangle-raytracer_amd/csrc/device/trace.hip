@@ -33,6 +33,7 @@
 #include "../host/bvh.hpp"
 #include "bzr.h"
 #include "patch_math.hpp"
+#include "emitter.hpp"
 
 using namespace bzr_dev;
 
@@ -65,6 +66,7 @@ struct bzr_mesh {
   float4 *leaf;     // 4 float4 per BVH leaf slot: the planar record, patch index in the last word
   uint32_t nnodes;
   float s_max;
+  float sphere[4];  // Ritter sphere over the gate-region boxes (bvh.cpp): the illumination pre-cull
 };
 
 struct bzr_ctx {
@@ -1150,6 +1152,7 @@ extern "C" bzr_status bzr_mesh_create(bzr_ctx *ctx, const void *patches, uint32_
   mesh->n = n;
   mesh->nnodes = static_cast<uint32_t>(bvh.nodes4.size());
   mesh->s_max = bvh.s_max;
+  for (int k = 0; k < 4; ++k) mesh->sphere[k] = bvh.sphere[k];
   struct Up {
     void **dst;
     const void *src;
@@ -1439,5 +1442,225 @@ extern "C" bzr_status bzr_mesh_interpolate(bzr_ctx *ctx, const bzr_mesh *mesh, i
   if (host) BZR_HIP(hipMemcpyAsync(out_xyz, d_out, ob, hipMemcpyDeviceToHost, ctx->stream));
   // the staged sub-triangle table must outlive the kernel: this call is synchronous
   BZR_HIP(hipStreamSynchronize(ctx->stream));
+  return BZR_OK;
+}
+
+// ------------------------------------------------------------ illumination
+namespace {
+// Rays first .. first+n-1 of the emitter into rays [6][ld].  With `status`: rays that cannot meet the
+// first lens's bounding sphere start as NONE (culled, never traced), the others INSIDE (the chain's
+// first refraction expects to enter the lens); stats[EMITTED], stats[CULLED] count them.
+__global__ __launch_bounds__(kBlock) void k_emit(bzr_emitter em, BeltTable bt, uint64_t first, uint32_t n, uint32_t ld,
+                                                 float *__restrict__ rays, uint32_t *__restrict__ patch,
+                                                 uint32_t *__restrict__ status, uint32_t *__restrict__ segments,
+                                                 float4 sphere, unsigned long long *__restrict__ stats) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  bool culled = false;
+  if (i < n) {
+    f3 o, d;
+    uint32_t p;
+    emit_ray(em, bt, first + i, o, d, p);
+    store_ray(rays, ld, i, o, d);
+    if (patch) patch[i] = p;
+    if (status) {
+      const float sp[4] = {sphere.x, sphere.y, sphere.z, sphere.w};
+      culled = !may_hit_sphere(o, d, sp);
+      status[i] = culled ? BZR_RR_NONE : BZR_RR_INSIDE;
+      if (segments) segments[i] = 0u;
+    }
+  }
+  if (stats) {
+    const unsigned long long made = __ballot(i < n), cut = __ballot(culled);
+    if ((threadIdx.x & 63u) == 0u) {
+      if (made) atomicAdd(&stats[BZR_ILLUM_EMITTED], (unsigned long long)__popcll(made));
+      if (cut) atomicAdd(&stats[BZR_ILLUM_CULLED], (unsigned long long)__popcll(cut));
+    }
+  }
+}
+
+// Rays that left the last lens (status OUTSIDE) meet the target plane: one count per landed ray.
+__global__ __launch_bounds__(kBlock) void k_land(bzr_target tg, float4 plane, float cell_u, float cell_v,
+                                                 const float *__restrict__ rays, uint32_t ld, uint32_t n,
+                                                 const uint32_t *__restrict__ status, uint32_t *__restrict__ hist,
+                                                 unsigned long long *__restrict__ stats) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  bool exited = false, landed = false;
+  if (i < n && status[i] == BZR_RR_OUTSIDE) {
+    exited = true;
+    f3 s, d;
+    load_ray(rays, ld, i, s, d);
+    const int32_t cell = target_cell(tg, mk(plane.x, plane.y, plane.z), plane.w, cell_u, cell_v, s, d);
+    if (cell >= 0) {
+      landed = true;
+      atomicAdd(&hist[cell], 1u);
+    }
+  }
+  const unsigned long long ex = __ballot(exited), la = __ballot(landed);
+  if ((threadIdx.x & 63u) == 0u) {
+    if (ex) atomicAdd(&stats[BZR_ILLUM_EXITED], (unsigned long long)__popcll(ex));
+    if (la) atomicAdd(&stats[BZR_ILLUM_LANDED], (unsigned long long)__popcll(la));
+  }
+}
+
+// UniformHemisphere(belts)'s patch table (reference/hostUtil.cpp:3-14, same float expressions) and the
+// belt boundaries cos(i * width) the device compares cos(incidence) against.
+bzr_status belt_tables(uint32_t belts, std::vector<float> &cos_lo, std::vector<uint32_t> &count,
+                       std::vector<uint32_t> &first) {
+  if (belts == 0 || belts > 4096) return set_error(BZR_ERR_INVALID_ARGUMENT, "belts must be 1..4096");
+  constexpr float kPi = 3.14159265358979323846f;  // cgPi, reference/3dGeomUtil.h:19
+  const float width = kPi / 2.0f / (float)belts;
+  cos_lo.assign(belts, 1.0f);
+  count.resize(belts);
+  first.resize(belts);
+  uint32_t so_far = 0;
+  for (uint32_t i = 0; i < belts; ++i) {
+    count[i] = (uint32_t)std::ceil(static_cast<double>(4.0f * (float)belts) *
+                                   std::sin(static_cast<double>((2.0f * (float)i + 1.0f) / (4.0f * (float)belts) * kPi)));
+    first[i] = so_far;
+    so_far += count[i];
+    if (i) cos_lo[i] = std::cos((float)i * width);
+  }
+  return BZR_OK;
+}
+
+bzr_status check_emitter(const bzr_emitter *em) {
+  if (!em) return set_error(BZR_ERR_INVALID_ARGUMENT, "null emitter");
+  if (!em->parts_u || !em->parts_v || !em->points_per_part || !em->rays_per_point)
+    return set_error(BZR_ERR_INVALID_ARGUMENT, "emitter counts must be positive");
+  return BZR_OK;
+}
+
+// The belt tables in device memory (carved from `st`), as the kernels' BeltTable.
+bzr_status upload_belts(bzr_ctx *ctx, const bzr_emitter *em, Staging &st, BeltTable &bt, std::vector<float> &cos_lo,
+                        std::vector<uint32_t> &count, std::vector<uint32_t> &first) {
+  if (bzr_status s = belt_tables(em->belts, cos_lo, count, first)) return s;
+  float *c = st.take<float>(em->belts);
+  uint32_t *k = st.take<uint32_t>(em->belts), *f = st.take<uint32_t>(em->belts);
+  BZR_HIP(hipMemcpyAsync(c, cos_lo.data(), em->belts * 4, hipMemcpyHostToDevice, ctx->stream));
+  BZR_HIP(hipMemcpyAsync(k, count.data(), em->belts * 4, hipMemcpyHostToDevice, ctx->stream));
+  BZR_HIP(hipMemcpyAsync(f, first.data(), em->belts * 4, hipMemcpyHostToDevice, ctx->stream));
+  bt = BeltTable{c, k, f, em->belts};
+  return BZR_OK;
+}
+size_t belt_bytes(uint32_t belts) { return 3 * round256((size_t)belts * 4); }
+}  // namespace
+
+extern "C" bzr_status bzr_mesh_bounding_sphere(const bzr_mesh *mesh, float out[4]) {
+  if (!mesh || !out) return set_error(BZR_ERR_INVALID_ARGUMENT, "null argument");
+  for (int k = 0; k < 4; ++k) out[k] = mesh->sphere[k];
+  return BZR_OK;
+}
+
+extern "C" bzr_status bzr_emit(bzr_ctx *ctx, const bzr_emitter *em, uint64_t first, uint32_t n, float *rays_soa,
+                               uint32_t *patch_index, uint32_t flags) {
+  if (!ctx) return set_error(BZR_ERR_INVALID_ARGUMENT, "null context");
+  if (bzr_status s = check_emitter(em)) return s;
+  if (n == 0) return BZR_OK;
+  if (!rays_soa) return set_error(BZR_ERR_INVALID_ARGUMENT, "null buffer");
+  DeviceGuard g(ctx->device);
+  const bool host = !(flags & BZR_DEVICE_PTRS);
+  const size_t rb = (size_t)n * 24, pb = (size_t)n * 4;
+  if (bzr_status s = ensure_buffer(ctx->scratch, ctx->scratch_bytes,
+                                   belt_bytes(em->belts) + (host ? round256(rb) + round256(pb) : 0)))
+    return s;
+  Staging st{static_cast<char *>(ctx->scratch)};
+  BeltTable bt;
+  std::vector<float> cos_lo;
+  std::vector<uint32_t> count, firsts;
+  if (bzr_status s = upload_belts(ctx, em, st, bt, cos_lo, count, firsts)) return s;
+  float *d_rays = host ? st.take<float>((size_t)n * 6) : rays_soa;
+  uint32_t *d_patch = host ? (patch_index ? st.take<uint32_t>(n) : nullptr) : patch_index;
+  hipLaunchKernelGGL(k_emit, dim3(grid_for(n)), dim3(kBlock), 0, ctx->stream, *em, bt, first, n, n, d_rays, d_patch,
+                     (uint32_t *)nullptr, (uint32_t *)nullptr, make_float4(0.0f, 0.0f, 0.0f, 0.0f),
+                     (unsigned long long *)nullptr);
+  BZR_HIP(hipGetLastError());
+  if (host) {
+    BZR_HIP(hipMemcpyAsync(rays_soa, d_rays, rb, hipMemcpyDeviceToHost, ctx->stream));
+    if (patch_index) BZR_HIP(hipMemcpyAsync(patch_index, d_patch, pb, hipMemcpyDeviceToHost, ctx->stream));
+  }
+  BZR_HIP(hipStreamSynchronize(ctx->stream));  // the staged belt tables must outlive the kernel
+  return BZR_OK;
+}
+
+extern "C" bzr_status bzr_illuminate(bzr_ctx *ctx, const bzr_mesh *const *lenses, const float *ri, uint32_t nlens,
+                                     const bzr_emitter *em, uint64_t total_rays, const bzr_target *tg, uint32_t *hist,
+                                     uint64_t stats[4], uint32_t flags) {
+  if (!ctx) return set_error(BZR_ERR_INVALID_ARGUMENT, "null context");
+  if (nlens == 0 || nlens > kMaxLenses) return set_error(BZR_ERR_INVALID_ARGUMENT, "nlens must be 1..8");
+  if (!lenses || !ri || !tg || !hist) return set_error(BZR_ERR_INVALID_ARGUMENT, "null argument");
+  if (bzr_status s = check_emitter(em)) return s;
+  if (!tg->bins_u || !tg->bins_v || !(tg->size_u > 0.0f) || !(tg->size_v > 0.0f))
+    return set_error(BZR_ERR_INVALID_ARGUMENT, "target bins and sizes must be positive");
+  LensSet set{};
+  set.count = nlens;
+  uint32_t nb = 0;
+  for (uint32_t l = 0; l < nlens; ++l) {
+    if (bzr_status s = check_ctx_mesh(ctx, lenses[l])) return s;
+    set.lens[l] = view_of(lenses[l], ri[l]);
+    nb = std::max(nb, set.lens[l].n);
+  }
+  DeviceGuard g(ctx->device);
+  // target plane (normal = axis_u x axis_v normalised, constant = n . origin) and cell sizes, in the
+  // oracle's operation order
+  const float *au = tg->axis_u, *av = tg->axis_v;
+  f3 pn{au[1] * av[2] - au[2] * av[1], au[2] * av[0] - au[0] * av[2], au[0] * av[1] - au[1] * av[0]};
+  {
+    const float z = pn.x * pn.x + (pn.y * pn.y + pn.z * pn.z);
+    if (z > 0.0f) {
+      const float s = std::sqrt(z);
+      pn = f3{pn.x / s, pn.y / s, pn.z / s};
+    }
+  }
+  const float pc = pn.x * tg->origin[0] + (pn.y * tg->origin[1] + pn.z * tg->origin[2]);
+  const float cell_u = tg->size_u / (float)tg->bins_u, cell_v = tg->size_v / (float)tg->bins_v;
+  const size_t cells = (size_t)tg->bins_u * tg->bins_v;
+  const bool host = !(flags & BZR_DEVICE_PTRS);
+  const uint32_t B = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(total_rays, 1), kChunk);
+  if (bzr_status s = ensure_buffer(ctx->scratch, ctx->scratch_bytes,
+                                   belt_bytes(em->belts) + round256((size_t)B * 24) + 2 * round256((size_t)B * 4) +
+                                       round256(32) + (host ? round256(cells * 4) : 0)))
+    return s;
+  Staging st{static_cast<char *>(ctx->scratch)};
+  BeltTable bt;
+  std::vector<float> cos_lo;
+  std::vector<uint32_t> count, firsts;
+  if (bzr_status s = upload_belts(ctx, em, st, bt, cos_lo, count, firsts)) return s;
+  float *d_rays = st.take<float>((size_t)B * 6);
+  uint32_t *d_st = st.take<uint32_t>(B), *d_seg = st.take<uint32_t>(B);
+  unsigned long long *d_stats = st.take<unsigned long long>(4);
+  uint32_t *d_hist = host ? st.take<uint32_t>(cells) : hist;
+  BZR_HIP(hipMemsetAsync(d_stats, 0, 32, ctx->stream));
+  if (host) BZR_HIP(hipMemsetAsync(d_hist, 0, cells * 4, ctx->stream));
+  Work w;
+  if (bzr_status s = ensure_work(ctx, B, nb, w)) return s;
+  const float4 sphere = make_float4(lenses[0]->sphere[0], lenses[0]->sphere[1], lenses[0]->sphere[2],
+                                    lenses[0]->sphere[3]);
+  for (uint64_t first = 0; first < total_rays; first += B) {
+    const uint32_t m = (uint32_t)std::min<uint64_t>(B, total_rays - first);
+    hipLaunchKernelGGL(k_emit, dim3(grid_for(m)), dim3(kBlock), 0, ctx->stream, *em, bt, first, m, B, d_rays,
+                       (uint32_t *)nullptr, d_st, d_seg, sphere, d_stats);
+    for (uint32_t l = 0; l < nlens; ++l)
+      for (uint32_t j = 0; j < 2; ++j) {
+        Out o{};
+        o.rays = d_rays;
+        o.expected_all = j == 0 ? uint32_t(BZR_RR_INSIDE) : uint32_t(BZR_RR_OUTSIDE);
+        o.status = d_st;
+        o.segments = d_seg;
+        o.ri = set.lens[l].ri;
+        if (bzr_status s = run_culled<kModeStage>(ctx, set.lens[l], d_rays, B, 0, m, d_st, o, w)) return s;
+      }
+    hipLaunchKernelGGL(k_land, dim3(grid_for(m)), dim3(kBlock), 0, ctx->stream, *tg, make_float4(pn.x, pn.y, pn.z, pc),
+                       cell_u, cell_v, d_rays, B, m, d_st, d_hist, d_stats);
+    BZR_HIP(hipGetLastError());
+  }
+  unsigned long long hs[4];
+  BZR_HIP(hipMemcpyAsync(hs, d_stats, 32, hipMemcpyDeviceToHost, ctx->stream));
+  std::vector<uint32_t> hh(host ? cells : 0);
+  if (host) BZR_HIP(hipMemcpyAsync(hh.data(), d_hist, cells * 4, hipMemcpyDeviceToHost, ctx->stream));
+  BZR_HIP(hipStreamSynchronize(ctx->stream));
+  if (host)
+    for (size_t k = 0; k < cells; ++k) hist[k] += hh[k];
+  if (stats)
+    for (int k = 0; k < 4; ++k) stats[k] = hs[k];
   return BZR_OK;
 }

@@ -281,7 +281,53 @@ Bvh build_bvh(const float *records, uint32_t n, uint32_t stride_words) {
     d[0] = b.lo[0]; d[1] = b.lo[1]; d[2] = b.lo[2]; d[3] = 0.0f;
     d[4] = b.hi[0]; d[5] = b.hi[1]; d[6] = b.hi[2]; d[7] = 0.0f;
   }
+  ritter_sphere(box, out.sphere);
   return out;
+}
+
+// Ritter's bounding sphere (the README's pre-cull, reference/README.md:194) over the corners of every
+// non-empty gate-region box: a ray that misses it cannot meet any gate region, so it passes no
+// planar gate.  Any non-finite corner disables the cull (radius +inf).  The radius is padded by
+// 1e-6 relative so the float-rounded centre and radius still enclose every corner.
+void ritter_sphere(std::vector<Box> const &box, float out[4]) {
+  std::vector<std::array<double, 3>> pts;
+  bool finite = true;
+  for (Box const &b : box) {
+    if (b.empty) continue;
+    for (int c = 0; c < 8; ++c) {
+      std::array<double, 3> p{(c & 1) ? b.hi[0] : b.lo[0], (c & 2) ? b.hi[1] : b.lo[1], (c & 4) ? b.hi[2] : b.lo[2]};
+      finite = finite && std::isfinite(p[0]) && std::isfinite(p[1]) && std::isfinite(p[2]);
+      pts.push_back(p);
+    }
+  }
+  out[0] = out[1] = out[2] = 0.0f;
+  out[3] = pts.empty() ? 0.0f : HUGE_VALF;
+  if (pts.empty() || !finite) return;
+  auto d2 = [](std::array<double, 3> const &a, std::array<double, 3> const &b) {
+    return (a[0] - b[0]) * (a[0] - b[0]) + (a[1] - b[1]) * (a[1] - b[1]) + (a[2] - b[2]) * (a[2] - b[2]);
+  };
+  auto farthest = [&](std::array<double, 3> const &from) {
+    size_t best = 0;
+    for (size_t i = 1; i < pts.size(); ++i)
+      if (d2(pts[i], from) > d2(pts[best], from)) best = i;
+    return pts[best];
+  };
+  std::array<double, 3> y = farthest(pts[0]), z = farthest(y);
+  std::array<double, 3> c{0.5 * (y[0] + z[0]), 0.5 * (y[1] + z[1]), 0.5 * (y[2] + z[2])};
+  double r = 0.5 * std::sqrt(d2(y, z));
+  for (auto const &p : pts) {  // grow to take every point outside (Ritter's second pass)
+    double d = std::sqrt(d2(p, c));
+    if (d > r) {
+      double nr = 0.5 * (r + d), k = (nr - r) / d;
+      for (int a = 0; a < 3; ++a) c[a] += (p[a] - c[a]) * k;
+      r = nr;
+    }
+  }
+  double need = 0.0;  // exact enclosing radius about the float-rounded centre
+  std::array<double, 3> cf{(double)(float)c[0], (double)(float)c[1], (double)(float)c[2]};
+  for (auto const &p : pts) need = std::max(need, std::sqrt(d2(p, cf)));
+  for (int a = 0; a < 3; ++a) out[a] = static_cast<float>(cf[a]);
+  out[3] = static_cast<float>(std::nextafter(need * (1.0 + 1e-6) + 1e-6, HUGE_VAL));
 }
 
 }  // namespace bzr_host
@@ -362,5 +408,12 @@ extern "C" int32_t bzr_debug_traverse(const void *patches, uint32_t n, uint32_t 
       }
     }
   }
+  return 0;
+}
+
+extern "C" int32_t bzr_debug_bounding_sphere(const void *patches, uint32_t n, uint32_t stride, float out[4]) {
+  if ((!patches && n) || !out || stride % 4 || stride < 264) return 1;
+  bzr_host::Bvh bvh = bzr_host::build_bvh(static_cast<const float *>(patches), n, stride / 4);
+  for (int k = 0; k < 4; ++k) out[k] = bvh.sphere[k];
   return 0;
 }

@@ -40,7 +40,10 @@ struct Bvh {
   std::vector<float> patch_box;    // per order slot: lo.xyz, 0, hi.xyz, 0 (the gate-region box)
   float extent = 0.0f;             // max |coordinate| of any finite box
   float s_max = 0.0f;              // rays with |origin|_inf > s_max take the brute-force path
+  float sphere[4] = {0, 0, 0, 0};  // Ritter sphere over the gate-region boxes: centre, radius
 };
+
+void ritter_sphere(std::vector<Box> const &box, float out[4]);
 
 // records: n patch records of stride_words floats (bzr_patch layout, 66 words)
 Bvh build_bvh(const float *records, uint32_t n, uint32_t stride_words);

@@ -173,6 +173,44 @@ bzr_status bzr_trace_chain(bzr_ctx *ctx, const bzr_mesh *const *lenses, const fl
 bzr_status bzr_mesh_interpolate(bzr_ctx *ctx, const bzr_mesh *mesh, int32_t divisor, float *out_xyz,
                                 uint32_t flags);
 
+/* ---- illumination: emitter -> lens chain -> target plane (reference README.md:159-194) ---- */
+/* A rectangular emitter (origin + a*edge_u + b*edge_v, a, b in [0,1)) divided into parts_u x
+ * parts_v parts; rays are numbered part by part, points_per_part points per part, rays_per_point
+ * rays per point.  Directions are uniform over the hemisphere around +x, sampled as
+ * UniformHemisphere::getRandom does (reference/hostUtil.cpp:16-29: cos(incidence) uniform in
+ * [0,1), turn uniform in [0, 2*pi)) from a counter-based generator (splitmix64 of seed and ray
+ * index), so any ray range can be generated independently; `belts` sets the hemisphere patch
+ * numbering of UniformHemisphere(belts) (reference/hostUtil.cpp:3-14). */
+typedef struct bzr_emitter {
+  float origin[3], edge_u[3], edge_v[3];
+  uint32_t parts_u, parts_v, points_per_part, rays_per_point, belts;
+  uint64_t seed;
+} bzr_emitter;
+/* The illuminated rectangle: origin + a*axis_u + b*axis_v (unit, orthogonal axes), a in
+ * [0, size_u), b in [0, size_v), bins_u x bins_v counting cells (row-major, u fastest).  A ray that
+ * leaves the last lens (status OUTSIDE) lands where Plane::intersect (reference/3dGeomUtil.h:279-296)
+ * meets the plane through origin with normal axis_u x axis_v. */
+typedef struct bzr_target {
+  float origin[3], axis_u[3], axis_v[3];
+  float size_u, size_v;
+  uint32_t bins_u, bins_v;
+} bzr_target;
+enum { BZR_ILLUM_EMITTED = 0, BZR_ILLUM_CULLED = 1, BZR_ILLUM_EXITED = 2, BZR_ILLUM_LANDED = 3 };
+/* Rays first .. first+n-1 of the emitter: rays_soa [6][n] (unit directions), hemisphere patch
+ * index per ray (may be NULL). */
+bzr_status bzr_emit(bzr_ctx *ctx, const bzr_emitter *em, uint64_t first, uint32_t n, float *rays_soa,
+                    uint32_t *patch_index, uint32_t flags);
+/* Emits `total_rays` rays, drops those that miss the first lens's bounding sphere (Ritter's sphere
+ * over the gate-region boxes: a ray that misses it cannot pass any planar gate, so dropping it is
+ * exact), traces the rest through the refraction chain and adds one count per landed ray to
+ * hist[bins_v][bins_u] (accumulates: zero it first).  stats (may be NULL) gets the BZR_ILLUM_*
+ * counts.  Synchronous; hist may be host or device memory per `flags`. */
+bzr_status bzr_illuminate(bzr_ctx *ctx, const bzr_mesh *const *lenses, const float *refractive_index,
+                          uint32_t nlens, const bzr_emitter *em, uint64_t total_rays, const bzr_target *target,
+                          uint32_t *hist, uint64_t stats[4], uint32_t flags);
+/* The bounding sphere bzr_illuminate culls with: center xyz, radius. */
+bzr_status bzr_mesh_bounding_sphere(const bzr_mesh *mesh, float out[4]);
+
 /* ---- host preprocessing (reference Mesh / BezierMesh construction) ---- */
 enum { BZR_ENVELOPE_ELLIPSOID = 0, BZR_ENVELOPE_TESTLENS = 1 };
 bzr_status bzr_trimesh_create(bzr_trimesh **out);

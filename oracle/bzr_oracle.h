@@ -172,6 +172,27 @@ uint32_t orc_to_which_side(ov3 start, ov3 end);
 ov3      orc_get_aperpendicular(ov3 v);
 float    orc_ray_average_error_squared(const oray *r, const ov3 *pts, uint32_t n);
 
+/* ---- illumination ends (illum_oracle.c) ---- */
+/* Same layouts as libbzr's bzr_emitter / bzr_target (include/bzr.h). */
+typedef struct {
+  float origin[3], edge_u[3], edge_v[3];
+  uint32_t parts_u, parts_v, points_per_part, rays_per_point, belts;
+  uint64_t seed;
+} orc_emitter;
+typedef struct {
+  float origin[3], axis_u[3], axis_v[3];
+  float size_u, size_v;
+  uint32_t bins_u, bins_v;
+} orc_target;
+typedef struct orc_hemisphere orc_hemisphere;   /* UniformHemisphere (reference/hostUtil.h:8-24) */
+orc_hemisphere *orc_hemisphere_create(uint32_t belts);
+void     orc_hemisphere_free(orc_hemisphere *h);
+uint32_t orc_hemisphere_patch_count(const orc_hemisphere *h);
+uint32_t orc_hemisphere_random(orc_hemisphere *h, float dir[3]);
+int      orc_emit(const orc_emitter *em, uint64_t first, uint32_t n, float *rays_soa, uint32_t *patch);
+void     orc_land(const orc_target *tg, const float *rays_soa, const uint32_t *status, uint32_t n, uint32_t *hist,
+                  uint64_t *exited, uint64_t *landed);
+
 #ifdef __cplusplus
 }
 #endif

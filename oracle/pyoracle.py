@@ -49,7 +49,8 @@ _MP = ctypes.POINTER(omesh)
 
 
 def build(force: bool = False) -> Path:
-    if force or not LIB_PATH.exists() or LIB_PATH.stat().st_mtime < (ORACLE_DIR / "bzr_oracle.c").stat().st_mtime:
+    newest = max((ORACLE_DIR / f).stat().st_mtime for f in ("bzr_oracle.c", "illum_oracle.c", "bzr_oracle.h"))
+    if force or not LIB_PATH.exists() or LIB_PATH.stat().st_mtime < newest:
         subprocess.run(["make", "-C", str(ORACLE_DIR)], check=True, capture_output=True)
     return LIB_PATH
 
@@ -89,6 +90,12 @@ def lib():
             "orc_counters": ([_P], None),
             "orc_planar_gate_batch": ([_P, ctypes.c_uint32, _P, ctypes.c_uint32, _P, ctypes.c_int], None),
             "orc_counters_reset": ([], None),
+            "orc_hemisphere_create": ([ctypes.c_uint32], _P),
+            "orc_hemisphere_free": ([_P], None),
+            "orc_hemisphere_patch_count": ([_P], ctypes.c_uint32),
+            "orc_hemisphere_random": ([_P, _P], ctypes.c_uint32),
+            "orc_emit": ([_P, ctypes.c_uint64, ctypes.c_uint32, _P, _P], ctypes.c_int),
+            "orc_land": ([_P, _P, _P, ctypes.c_uint32, _P, _P, _P], None),
             "orc_plane_from_1proportion_2points": ([ctypes.c_float, ov3, ov3], oplane),
             "orc_plane_from_3points": ([ov3, ov3, ov3], oplane),
             "orc_plane_from_1vector_2points": ([ov3, ov3, ov3], oplane),
@@ -317,3 +324,62 @@ def measure_approximation(split_steps, sectors, belts, size, divisor) -> float:
     if rc:
         raise RuntimeError(_err())
     return e.value
+
+
+# ------------------------------------------------------------------ illumination ends (illum_oracle.c)
+class Emitter(ctypes.Structure):
+    """orc_emitter (same layout as libbzr's bzr_emitter)."""
+    _fields_ = [("origin", ctypes.c_float * 3), ("edge_u", ctypes.c_float * 3), ("edge_v", ctypes.c_float * 3),
+                ("parts_u", ctypes.c_uint32), ("parts_v", ctypes.c_uint32), ("points_per_part", ctypes.c_uint32),
+                ("rays_per_point", ctypes.c_uint32), ("belts", ctypes.c_uint32), ("seed", ctypes.c_uint64)]
+
+
+class Target(ctypes.Structure):
+    """orc_target (same layout as libbzr's bzr_target)."""
+    _fields_ = [("origin", ctypes.c_float * 3), ("axis_u", ctypes.c_float * 3), ("axis_v", ctypes.c_float * 3),
+                ("size_u", ctypes.c_float), ("size_v", ctypes.c_float), ("bins_u", ctypes.c_uint32),
+                ("bins_v", ctypes.c_uint32)]
+
+
+def emit(em: Emitter, first: int, n: int):
+    """Rays first .. first+n-1 of the counter-based emitter -> (rays [6, n], hemisphere patch [n])."""
+    rays = np.empty((6, n), np.float32)
+    patch = np.empty(n, np.uint32)
+    if lib().orc_emit(ctypes.byref(em), first, n, rays.ctypes.data, patch.ctypes.data):
+        raise RuntimeError("orc_emit: bad emitter")
+    return rays, patch
+
+
+def land(tg: Target, rays: np.ndarray, status: np.ndarray, hist: np.ndarray | None = None):
+    """Bin the rays with status OUTSIDE on the target -> (hist [bins_v, bins_u] uint32, exited, landed)."""
+    r = np.ascontiguousarray(rays, np.float32)
+    s = np.ascontiguousarray(status, np.uint32)
+    h = np.zeros((tg.bins_v, tg.bins_u), np.uint32) if hist is None else hist
+    ex, la = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    lib().orc_land(ctypes.byref(tg), r.ctypes.data, s.ctypes.data, r.shape[1], h.ctypes.data, ctypes.byref(ex),
+                   ctypes.byref(la))
+    return h, ex.value, la.value
+
+
+class Hemisphere:
+    """UniformHemisphere (reference/hostUtil.cpp) with the reference's std::ranlux24_base stream."""
+
+    def __init__(self, belts: int):
+        self.h = lib().orc_hemisphere_create(belts)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_hemisphere_free(self.h)
+            self.h = None
+
+    @property
+    def patch_count(self) -> int:
+        return lib().orc_hemisphere_patch_count(self.h)
+
+    def random(self, n: int):
+        """n draws of getRandom() -> (directions [n, 3] float32, patch indices [n])."""
+        d = np.empty((n, 3), np.float32)
+        idx = np.empty(n, np.uint32)
+        for k in range(n):
+            idx[k] = lib().orc_hemisphere_random(self.h, d[k].ctypes.data)
+        return d, idx

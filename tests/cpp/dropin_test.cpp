@@ -15,6 +15,7 @@
 #include "bezierLens.h"
 #include "bezierMesh.h"
 #include "mesh.h"
+#include "hostUtil.h"
 #include "bzr_oracle.h"
 
 static int g_fail = 0, g_checks = 0;
@@ -194,7 +195,28 @@ static void hot_path(Mesh const &lensMesh) {
   std::printf("hot path: %d hits, %d exits of %zu rays\n", hits, exits, rays.size());
 }
 
+// UniformHemisphere (reference/hostUtil.cpp) through the drop-in header vs the oracle's restatement of
+// the same std::ranlux24_base stream: patch counts and the first 5000 draws, bit for bit.
+static void hemisphere() {
+  for (uint32_t belts : {1u, 3u, 8u, 16u}) {
+    UniformHemisphere h(belts);
+    orc_hemisphere *o = orc_hemisphere_create(belts);
+    CHECK(h.getPatchCount() == orc_hemisphere_patch_count(o));
+    int same = 0;
+    for (int k = 0; k < 5000; ++k) {
+      auto [d, idx] = h.getRandom();
+      float od[3];
+      uint32_t oidx = orc_hemisphere_random(o, od);
+      same += std::memcmp(&d(0), &od[0], 4) == 0 && std::memcmp(&d(1), &od[1], 4) == 0 &&
+              std::memcmp(&d(2), &od[2], 4) == 0 && idx == oidx && idx < h.getPatchCount();
+    }
+    CHECK(same == 5000);
+    orc_hemisphere_free(o);
+  }
+}
+
 int main() {
+  hemisphere();
   l1_geometry();
   Mesh lens;
   preprocessing(lens);

@@ -106,3 +106,26 @@ def test_ill_conditioned_patches(bzr, orc):
     d /= np.linalg.norm(d, axis=1, keepdims=True)
     rays = np.concatenate([rays, np.concatenate([o.T, d.T]).astype(np.float32)], 1)
     check(bzr, orc, patches, rays)
+
+
+@pytest.mark.parametrize("cfg_name", ["cfg1", "cfg2", "cfg3"])
+def test_bounding_sphere_encloses_gate_boxes(bzr, cfg_name):
+    """bzr_illuminate's pre-cull is exact only if the sphere holds every gate-region box: check all
+    eight corners of every non-empty box (in double, against the float centre and radius)."""
+    patches = build_lens(bzr.TriMesh, CONFIGS[cfg_name].lenses[0]).bezier_patches()
+    boxes, _ = gate_boxes(bzr, patches)
+    L = bzr.lib()
+    fn = L.bzr_debug_bounding_sphere
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]
+    fn.restype = ctypes.c_int32
+    sph = np.zeros(4, np.float32)
+    p = np.ascontiguousarray(patches, np.float32)
+    assert fn(p.ctypes.data, len(p), 264, sph.ctypes.data) == 0
+    lo, hi = boxes[:, :3].astype(np.float64), boxes[:, 3:].astype(np.float64)
+    keep = (lo <= hi).all(axis=1)
+    assert keep.sum() > 0 and np.isfinite(sph).all()
+    corners = np.stack([np.where([(c >> a) & 1 for a in range(3)], hi[keep], lo[keep]) for c in range(8)])
+    dist = np.linalg.norm(corners - sph[:3].astype(np.float64), axis=2)
+    assert dist.max() <= float(sph[3])
+    # and it is a useful cull: not much larger than the boxes' own extent
+    assert float(sph[3]) < 1.5 * 0.5 * np.linalg.norm(hi[keep].max(0) - lo[keep].min(0)) + 1e-3
