@@ -95,7 +95,10 @@ namespace {
 constexpr int kBlock = 256;
 constexpr int kWaves = kBlock / 64;
 constexpr uint32_t kMaxLenses = 8;
-constexpr uint32_t kMaxCand = 16;        // candidate list length per ray and segment
+#ifndef BZR_MAX_CAND
+#define BZR_MAX_CAND 24
+#endif
+constexpr uint32_t kMaxCand = BZR_MAX_CAND;  // candidate list length per ray and segment
 constexpr uint32_t kOverflow = 0xFFFFu;  // count value: resolve with the full scan
 constexpr int kStack = 64;
 
@@ -116,6 +119,10 @@ __device__ __forceinline__ uint32_t xcd_contiguous(uint32_t b, uint32_t nblocks)
 #define BZR_TRAV_BLOCK 256
 #endif
 constexpr int kTravBlock = BZR_TRAV_BLOCK;
+// BZR_SLAB_FMA (default 1): the traversal slab test as fma(lo, inv, -s*inv) (mirrored by bvh.cpp slab_h).
+#ifndef BZR_SLAB_FMA
+#define BZR_SLAB_FMA 1
+#endif
 // BZR_NEWTON_XCD (default 1): k_newton waves take chunks in XCD-contiguous order (scalar-cache reuse).
 #ifndef BZR_NEWTON_XCD
 #define BZR_NEWTON_XCD 0
@@ -271,10 +278,21 @@ __device__ __forceinline__ float safe_inv(float x) {
   return 1.0f / (fabsf(x) < 1e-20f ? copysignf(1e-20f, x) : x);
 }
 
-__device__ __forceinline__ bool slab(float4 lo, float4 hi, f3 s, f3 inv) {
+// Slab test of the ray (origin s, per-axis reciprocal direction inv, sinv = s * inv) against a box.
+// Conservative only (the gate-region boxes are padded for its rounding, bvh.cpp): with FMA each
+// plane distance is one fma(lo, inv, -s*inv), error <= (|s| + |t|) * 2^-23 < the pad.
+__device__ __forceinline__ bool slab(float4 lo, float4 hi, f3 s, f3 sinv, f3 inv) {
+#if BZR_SLAB_FMA
+  (void)s;
+  float ax = __builtin_fmaf(lo.x, inv.x, -sinv.x), bx = __builtin_fmaf(hi.x, inv.x, -sinv.x);
+  float ay = __builtin_fmaf(lo.y, inv.y, -sinv.y), by = __builtin_fmaf(hi.y, inv.y, -sinv.y);
+  float az = __builtin_fmaf(lo.z, inv.z, -sinv.z), bz = __builtin_fmaf(hi.z, inv.z, -sinv.z);
+#else
+  (void)sinv;
   float ax = (lo.x - s.x) * inv.x, bx = (hi.x - s.x) * inv.x;
   float ay = (lo.y - s.y) * inv.y, by = (hi.y - s.y) * inv.y;
   float az = (lo.z - s.z) * inv.z, bz = (hi.z - s.z) * inv.z;
+#endif
   float tnear = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
   float tfar = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
   return tnear <= tfar && tfar >= 0.0f;
@@ -383,7 +401,8 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
     cnt = kOverflow;
     active = false;
   }
-  f3 inv = mk(safe_inv(d.x), safe_inv(d.y), safe_inv(d.z));
+  const f3 inv = mk(safe_inv(d.x), safe_inv(d.y), safe_inv(d.z));
+  const f3 sinv = mk(s.x * inv.x, s.y * inv.y, s.z * inv.z);
   int sp = 0;
   if (m.n > 0 && __any(active)) {
     stk[0] = 0u;
@@ -402,7 +421,7 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
       const float4 lo = make_float4(__uint_as_float(na[c]), __uint_as_float(na[4 + c]), __uint_as_float(na[8 + c]), 0.0f);
       const float4 hi = make_float4(__uint_as_float(na[12 + c]), __uint_as_float(nb[c]), __uint_as_float(nb[4 + c]), 0.0f);
       ch[c] = nb[8 + c];
-      hit[c] = active & (ch[c] != bzr_host::kEmptyChild) & slab(lo, hi, s, inv);
+      hit[c] = active & (ch[c] != bzr_host::kEmptyChild) & slab(lo, hi, s, sinv, inv);
     }
 #pragma unroll
     for (int c = 0; c < 4; ++c) {

@@ -349,12 +349,13 @@ extern "C" int32_t bzr_debug_gate_boxes(const void *patches, uint32_t n, uint32_
 
 namespace {
 float safe_inv_h(float x) { return 1.0f / (std::fabs(x) < 1e-20f ? std::copysign(1e-20f, x) : x); }
-// same operation order as the device slab() in trace.hip
+// same operation order as the device slab() in trace.hip (BZR_SLAB_FMA: fma(lo, inv, -s*inv))
 bool slab_h(const float lo[3], const float hi[3], const float s[3], const float inv[3]) {
   float a[3], b[3];
   for (int k = 0; k < 3; ++k) {
-    a[k] = (lo[k] - s[k]) * inv[k];
-    b[k] = (hi[k] - s[k]) * inv[k];
+    const float sinv = s[k] * inv[k];
+    a[k] = std::fma(lo[k], inv[k], -sinv);
+    b[k] = std::fma(hi[k], inv[k], -sinv);
   }
   float tnear = std::fmax(std::fmax(std::fmin(a[0], b[0]), std::fmin(a[1], b[1])), std::fmin(a[2], b[2]));
   float tfar = std::fmin(std::fmin(std::fmax(a[0], b[0]), std::fmax(a[1], b[1])), std::fmax(a[2], b[2]));

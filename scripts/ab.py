@@ -105,11 +105,21 @@ def main():
                 if calls[k]:
                     r["kern"].setdefault(name, []).append(ms[k] / a.steps)
     segs = int(ref["sg"].sum().item())
+    for r in runs:  # work counters of one frame
+        h, ctx = r["h"], r["ctx"]
+        cnt = (ctypes.c_uint64 * 8)()
+        h.bzr_ctx_counters(ctx, 1)
+        h.bzr_ctx_counters_report(ctx, cnt)
+        r["step"]()
+        h.bzr_ctx_counters_report(ctx, cnt)
+        h.bzr_ctx_counters(ctx, 0)
+        r["counters"] = {k: int(cnt[i]) for i, k in enumerate(bzr_amd.COUNTERS)}
     for r in runs:
         med = statistics.median(r["times"])
         print(json.dumps({"variant": r["name"], "same_as_first": r["same"], "ms_median": round(med, 4),
                           "ms_min": round(min(r["times"]), 4), "mrays_s": round(segs / med / 1e3, 1),
-                          "kernels_ms_per_step": {k: round(statistics.median(v), 4) for k, v in r["kern"].items()}}),
+                          "kernels_ms_per_step": {k: round(statistics.median(v), 4) for k, v in r["kern"].items()},
+                          "counters": r["counters"]}),
               flush=True)
 
 
