@@ -127,9 +127,9 @@ constexpr int kTravBlock = BZR_TRAV_BLOCK;
 #ifndef BZR_NEWTON_XCD
 #define BZR_NEWTON_XCD 0
 #endif
-// Blocks of k_overflow (one overflow ray per block at a time, grid-stride over the list).
+// Blocks of k_overflow (grid-stride over (overflow ray, patch slice) items).
 #ifndef BZR_OVERFLOW_BLOCKS
-#define BZR_OVERFLOW_BLOCKS 256u
+#define BZR_OVERFLOW_BLOCKS 2048u
 #endif
 // BZR_NEWTON_GATED (default 1): k_newton skips the planar gate its pairs already passed in k_traverse.
 #ifndef BZR_NEWTON_GATED
@@ -309,8 +309,8 @@ __device__ __forceinline__ bool slab(float4 lo, float4 hi, f3 s, f3 sinv, f3 inv
 //               time with the patch record in scalar registers (uniform loads); hits go to a per-pair
 //               slot and a per-ray 64-bit atomicMin on (t order key, pair index)
 //   k_follow    follow-side results: the named neighbour with cNone, per lane
-//   k_finish    winner -> BezierIntersection / refraction, for rays not on the overflow list
-//   k_overflow  the reference's in-order scan for the overflow list
+//   k_overflow  the reference's in-order scan for the overflow list, sliced over patches -> key
+//   k_finish    winner -> BezierIntersection / refraction (overflow rays: their winner re-evaluated)
 // Pair indices are patch-major, so for one ray (t, pair index) orders like (t, scanned patch
 // index): the atomicMin winner is the reference's strict-< in-order winner.
 struct Work {
@@ -652,19 +652,20 @@ __global__ __launch_bounds__(kBlock) void k_follow(MeshView m, const float *__re
 }
 
 template <int kMode>
-__global__ __launch_bounds__(kBlock) void k_finish(const float *rays, uint32_t ld, uint32_t off, uint32_t n, Work w,
-                                                   Out o) {
+__global__ __launch_bounds__(kBlock) void k_finish(MeshView m, const float *rays, uint32_t ld, uint32_t off, uint32_t n,
+                                                   Work w, Out o) {
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
   const uint32_t gi = off + i;
   if (kMode == kModeStage && o.status[gi] == BZR_RR_NONE) return;
-  if (w.count[i] > kMaxCand) return;  // k_overflow
   f3 s, d;
   load_ray(rays, ld, gi, s, d);
   Hit h = no_hit();
   uint32_t patch = 0xFFFFFFFFu;
   const unsigned long long k = w.key[i];
-  if (k != ~0ull) {
+  if (w.count[i] > kMaxCand) {  // overflow ray: k_overflow left (t order, scanned patch) -- evaluate it again
+    if (k != ~0ull) h = evaluate_patch(m, static_cast<uint32_t>(k), s, d, patch);
+  } else if (k != ~0ull) {
     const uint32_t p = static_cast<uint32_t>(k);
 
     const float4 *r = reinterpret_cast<const float4 *>(w.slot) + (size_t)3 * p;  // AoS: 48 bytes per pair
@@ -680,9 +681,14 @@ __global__ __launch_bounds__(kBlock) void k_finish(const float *rays, uint32_t l
   emit<kMode>(o, ld, gi, s, d, h, patch);
 }
 
-// The rays k_traverse could not take, one block per ray: thread t scans patches t, t+256, ... in
-// index order (strict <, so per thread the lowest index wins ties), then the block takes the
-// (t, index) lexicographic minimum -- the winner of the reference's single in-order scan.
+// The rays k_traverse could not take: the reference's full in-order scan, split into
+// (overflow ray, patch slice) items so a few rays over a large mesh still fill the chip.  Each thread
+// scans patches t, t+256, ... of its slice (strict <: per thread the lowest index wins ties), and each
+// wave folds its (t order, patch index) lexicographic minimum into the ray's key with one atomicMin:
+// the winner of the reference's single in-order scan.  k_finish evaluates the winning patch again
+// (same arithmetic, same bits) and emits it.  (Waves walking a slice with scalar-loaded records for
+// 64 rays at once, as k_intersect_scan does, measured 4x slower: the serial walk waits on each load.)
+constexpr uint32_t kOvfSlice = kBlock * 8;  // patches per item
 __device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v) {
 #pragma unroll
   for (int k = 32; k >= 1; k >>= 1) {
@@ -692,42 +698,30 @@ __device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v)
   return v;
 }
 
-template <int kMode>
-__global__ __launch_bounds__(kBlock) void k_overflow(MeshView m, const float *rays, uint32_t ld, uint32_t off, Work w,
-                                                     Out o) {
-  __shared__ unsigned long long red[kWaves];
+__global__ __launch_bounds__(kBlock) void k_overflow(MeshView m, const float *rays, uint32_t ld, uint32_t off, Work w) {
   const uint32_t V = __builtin_amdgcn_readfirstlane(w.ctr[1]);
-  for (uint32_t q = blockIdx.x; q < V; q += gridDim.x) {
-    const uint32_t gi = off + w.ovf[q];
+  const uint32_t S = (m.n + kOvfSlice - 1) / kOvfSlice;
+  for (uint32_t item = blockIdx.x; item < V * S; item += gridDim.x) {
+    const uint32_t q = item / S, lo = (item - q * S) * kOvfSlice, hi = min(m.n, lo + kOvfSlice);
+    const uint32_t i = w.ovf[q];
     f3 s, d;
-    load_ray(rays, ld, gi, s, d);
-    Hit best = no_hit();
-    uint32_t best_b = 0xFFFFFFFFu, best_src = 0xFFFFFFFFu;
+    load_ray(rays, ld, off + i, s, d);
+    float best_t = FLT_MAX;
+    uint32_t best_b = 0xFFFFFFFFu;
 #pragma unroll 4
-    for (uint32_t b = threadIdx.x; b < m.n; b += kBlock) {
+    for (uint32_t b = lo + threadIdx.x; b < hi; b += kBlock) {
       const float4 *qq = m.planar + 4u * b;
       if (!planar_gate(qq[0], qq[1], qq[2], qq[3], s, d)) continue;
       uint32_t src;
       Hit h = evaluate_patch(m, b, s, d, src);
-      if (h.what == kIntersect && h.t < best.t) {
-        best = h;
+      if (h.what == kIntersect && h.t < best_t) {
+        best_t = h.t;
         best_b = b;
-        best_src = src;
       }
     }
-    const unsigned long long mine =
-        best_b != 0xFFFFFFFFu ? ((unsigned long long)t_order(best.t) << 32) | best_b : ~0ull;
-    unsigned long long win = wave_min_u64(mine);
-    if ((threadIdx.x & 63u) == 0) red[threadIdx.x >> 6] = win;
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < kWaves; ++k) win = red[k] < win ? red[k] : win;
-    __syncthreads();  // red is reused by the next ray
-    if (win == ~0ull) {
-      if (threadIdx.x == 0) emit<kMode>(o, ld, gi, s, d, no_hit(), 0xFFFFFFFFu);
-    } else if (mine == win) {
-      emit<kMode>(o, ld, gi, s, d, best, best_src);
-    }
+    const unsigned long long win =
+        wave_min_u64(best_b != 0xFFFFFFFFu ? ((unsigned long long)t_order(best_t) << 32) | best_b : ~0ull);
+    if ((threadIdx.x & 63u) == 0 && win != ~0ull) atomicMin(&w.key[i], win);
   }
 }
 
@@ -998,9 +992,12 @@ bzr_status run_culled(bzr_ctx *ctx, const MeshView &mv, const float *rays, uint3
          mv.full, w.offs + hn, w.pairs, w.slot, w.cap, w.key, w.fol, w.ctr, w.lanes, w.ctr + 3);
   launch(ctx, BZR_KERNEL_FOLLOW, k_follow, dim3(std::min<uint32_t>(grid_for(n / 8 + 1), 1024u)), mv, rays, ld, off,
          w);
-  launch(ctx, BZR_KERNEL_FINISH, k_finish<kMode>, dim3(grid_for(n)), rays, ld, off, n, w, o);
-  launch(ctx, BZR_KERNEL_OVERFLOW, k_overflow<kMode>, dim3(std::min<uint32_t>(n, BZR_OVERFLOW_BLOCKS)), mv, rays, ld, off,
-         w, o);
+  {  // overflow rays' keys are untouched by the Newton stage (their lists are empty)
+    const uint32_t items = n * ((nb + kOvfSlice - 1) / kOvfSlice);
+    launch(ctx, BZR_KERNEL_OVERFLOW, k_overflow, dim3(std::max<uint32_t>(std::min<uint32_t>(items, BZR_OVERFLOW_BLOCKS), 1u)),
+           mv, rays, ld, off, w);
+  }
+  launch(ctx, BZR_KERNEL_FINISH, k_finish<kMode>, dim3(grid_for(n)), mv, rays, ld, off, n, w, o);
   if (ctx->counting && ctx->counters)
     hipLaunchKernelGGL(k_count, dim3(1), dim3(64), 0, ctx->stream, w, nb, ctx->counters);
   BZR_HIP(hipGetLastError());

@@ -138,11 +138,91 @@ Box gate_region_box(const float *rec, double s_max) {
   return bx;
 }
 
+#ifndef BZR_BVH_SAH
+#define BZR_BVH_SAH 1
+#endif
+
 struct Builder {
   std::vector<Box> const &box;
   std::vector<std::array<float, 3>> centre;
   std::vector<uint32_t> &order;
   std::vector<BvhNode> &nodes;
+
+  // Binned surface-area-heuristic split of order[first, first+count) (16 centroid bins per axis):
+  // minimises sum over both sides of (box half-area x patches).  The gate-region boxes differ in
+  // size by orders of magnitude (ill-conditioned patches have huge ones), which a median split
+  // spreads over many subtrees.  Returns the left side's size after partitioning, 0 for "no useful
+  // split" (the caller falls back to the median).  Any split keeps the culling exact.
+  uint32_t sah_split(uint32_t first, uint32_t count, std::array<float, 3> const &clo, std::array<float, 3> const &chi) {
+    constexpr int kBins = 16;
+    constexpr double kHuge = 1e30;
+    auto area = [](std::array<double, 3> const &lo, std::array<double, 3> const &hi) {
+      double e[3];
+      for (int a = 0; a < 3; ++a) e[a] = std::max(0.0, hi[a] - lo[a]);
+      double s = e[0] * e[1] + e[1] * e[2] + e[2] * e[0];
+      return std::isfinite(s) ? s : kHuge;
+    };
+    double best = HUGE_VAL;
+    int best_axis = -1, best_bin = 0;
+    for (int a = 0; a < 3; ++a) {
+      const double ext = (double)chi[a] - (double)clo[a];
+      if (!(ext > 0.0) || !std::isfinite(ext)) continue;
+      struct Bin {
+        std::array<double, 3> lo{HUGE_VAL, HUGE_VAL, HUGE_VAL}, hi{-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
+        uint32_t n = 0;
+      } bins[kBins];
+      for (uint32_t k = first; k < first + count; ++k) {
+        const uint32_t p = order[k];
+        int b = (int)((centre[p][a] - (double)clo[a]) / ext * kBins);
+        b = std::min(std::max(b, 0), kBins - 1);
+        bins[b].n++;
+        if (box[p].empty) continue;
+        for (int d = 0; d < 3; ++d) {
+          bins[b].lo[d] = std::min(bins[b].lo[d], (double)box[p].lo[d]);
+          bins[b].hi[d] = std::max(bins[b].hi[d], (double)box[p].hi[d]);
+        }
+      }
+      // sweep: right-side areas / counts from the top, then left side from the bottom
+      double right_area[kBins];
+      uint32_t right_n[kBins];
+      std::array<double, 3> lo{HUGE_VAL, HUGE_VAL, HUGE_VAL}, hi{-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
+      uint32_t nr = 0;
+      for (int b = kBins - 1; b > 0; --b) {
+        for (int d = 0; d < 3; ++d) {
+          lo[d] = std::min(lo[d], bins[b].lo[d]);
+          hi[d] = std::max(hi[d], bins[b].hi[d]);
+        }
+        nr += bins[b].n;
+        right_area[b] = area(lo, hi);
+        right_n[b] = nr;
+      }
+      lo = {HUGE_VAL, HUGE_VAL, HUGE_VAL};
+      hi = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
+      uint32_t nl = 0;
+      for (int b = 1; b < kBins; ++b) {  // split between bin b-1 and b
+        for (int d = 0; d < 3; ++d) {
+          lo[d] = std::min(lo[d], bins[b - 1].lo[d]);
+          hi[d] = std::max(hi[d], bins[b - 1].hi[d]);
+        }
+        nl += bins[b - 1].n;
+        if (nl == 0 || right_n[b] == 0) continue;
+        const double cost = area(lo, hi) * nl + right_area[b] * right_n[b];
+        if (cost < best) {
+          best = cost;
+          best_axis = a;
+          best_bin = b;
+        }
+      }
+    }
+    if (best_axis < 0) return 0;
+    const double ext = (double)chi[best_axis] - (double)clo[best_axis];
+    auto mid = std::partition(order.begin() + first, order.begin() + first + count, [&](uint32_t p) {
+      int b = (int)((centre[p][best_axis] - (double)clo[best_axis]) / ext * kBins);
+      return std::min(std::max(b, 0), kBins - 1) < best_bin;
+    });
+    const uint32_t cut = static_cast<uint32_t>(mid - (order.begin() + first));
+    return (cut == 0 || cut == count) ? 0u : cut;
+  }
 
   uint32_t build(uint32_t first, uint32_t count) {
     uint32_t id = static_cast<uint32_t>(nodes.size());
@@ -171,6 +251,16 @@ struct Builder {
       nodes[id] = nd;
       return id;
     }
+#if BZR_BVH_SAH
+    if (uint32_t cut = sah_split(first, count, clo, chi)) {
+      uint32_t left = build(first, cut);
+      uint32_t right = build(first + cut, count - cut);
+      nd.a = left;
+      nd.b = right;
+      nodes[id] = nd;
+      return id;
+    }
+#endif
     int axis = 0;
     for (int a = 1; a < 3; ++a)
       if (chi[a] - clo[a] > chi[axis] - clo[axis]) axis = a;

@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--config", default="cfg2")
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--side", type=int, default=0, help="rays per image side (0 = the config's own)")
     a = ap.parse_args()
     import torch
 
@@ -45,7 +46,7 @@ def main():
     cfg = CONFIGS[a.config]
     patches = [build_lens(bzr_amd.TriMesh, l).bezier_patches() for l in cfg.lenses]
     ris = (ctypes.c_float * len(patches))(*[l.ri for l in cfg.lenses])
-    rays = torch.from_numpy(grid_rays(cfg)).cuda()
+    rays = torch.from_numpy(grid_rays(cfg, side=a.side) if a.side else grid_rays(cfg)).cuda()
     n = rays.shape[1]
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
@@ -63,15 +64,25 @@ def main():
             assert h.bzr_mesh_create(ctx, pa.ctypes.data, len(pa), 264, ctypes.byref(m)) == 0, h.bzr_last_error()
             meshes.append(m)
         marr = (ctypes.c_void_p * len(meshes))(*[m.value for m in meshes])
-        out = torch.empty((6, n), dtype=torch.float32, device="cuda")
-        st = torch.empty(n, dtype=torch.int32, device="cuda")
-        sg = torch.empty(n, dtype=torch.int32, device="cuda")
+        if cfg.op == "chain":
+            out = torch.empty((6, n), dtype=torch.float32, device="cuda")
+            st = torch.empty(n, dtype=torch.int32, device="cuda")
+            sg = torch.empty(n, dtype=torch.int32, device="cuda")
 
-        def step(h=h, ctx=ctx, marr=marr, out=out, st=st, sg=sg):
-            r = h.bzr_trace_chain(ctx, marr, ris, len(patches), ctypes.c_void_p(rays.data_ptr()), n,
-                                  ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(st.data_ptr()),
-                                  ctypes.c_void_p(sg.data_ptr()), bzr_amd.DEVICE_PTRS)
-            assert r == 0, h.bzr_last_error()
+            def step(h=h, ctx=ctx, marr=marr, out=out, st=st, sg=sg):
+                r = h.bzr_trace_chain(ctx, marr, ris, len(patches), ctypes.c_void_p(rays.data_ptr()), n,
+                                      ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(st.data_ptr()),
+                                      ctypes.c_void_p(sg.data_ptr()), bzr_amd.DEVICE_PTRS)
+                assert r == 0, h.bzr_last_error()
+        else:  # BezierMesh::intersect configs (cfg3, cfg5): one segment per ray
+            out = torch.empty((13, n), dtype=torch.float32, device="cuda")
+            st = torch.zeros(1, dtype=torch.int32, device="cuda")
+            sg = torch.ones(n, dtype=torch.int32, device="cuda")
+
+            def step(h=h, ctx=ctx, m=meshes[0], out=out):
+                r = h.bzr_intersect(ctx, m, ctypes.c_void_p(rays.data_ptr()), n, ctypes.c_void_p(out.data_ptr()),
+                                    bzr_amd.DEVICE_PTRS)
+                assert r == 0, h.bzr_last_error()
         for _ in range(3):
             step()
         torch.cuda.synchronize()

@@ -58,7 +58,17 @@ def run(name, side, reps):
         step()
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / reps
-    extra = {}
+    ctx.timing(True)  # per-kernel HIP-event times in a separate, untimed repetition
+    ctx.timing_report()
+    step()
+    kern = {k: round(ms, 3) for k, (ms, calls) in ctx.timing_report().items()}
+    ctx.timing(False)
+    ctx.counters(True)
+    ctx.counters_report()
+    step()
+    cnt = ctx.counters_report()
+    ctx.counters(False)
+    extra = {"kernels_ms": kern, "counters": cnt}
     if g is None:
         extra["hit_fraction"] = round(float((hits[11].view(torch.int32) == 4).float().mean().item()), 4)
     print(json.dumps({"config": name, "rays_side": side, "patches": int(sum(len(p) for p in patches)),

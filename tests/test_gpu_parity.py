@@ -250,6 +250,18 @@ def test_culled_equals_bruteforce_robot_and_random(bzr, orc, ctx, meshes):
     a = bzr.intersect(ctx, dm, rays)
     b = bzr.intersect(ctx, dm, rays, mode=bzr.ACCEL_NONE)
     assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    # far origins on the robot mesh: every ray takes the overflow scan, which splits the 28800 patches
+    # into 15 slices per ray (k_overflow), so the cross-slice (t, patch) minimum is exercised
+    rng = np.random.default_rng(22)
+    lo, hi = meshes["cfg3"][0][:, 19:49].reshape(-1, 3).min(0), meshes["cfg3"][0][:, 19:49].reshape(-1, 3).max(0)
+    tgt = rng.uniform(lo, hi, (20000, 3))
+    o = tgt + rng.normal(size=(20000, 3)) * 1e4 * np.abs(hi - lo).max()
+    d = (tgt - o) / np.linalg.norm(tgt - o, axis=1, keepdims=True)
+    far = np.concatenate([o.T, d.T]).astype(np.float32)
+    a = bzr.intersect(ctx, dm, far)
+    b = bzr.intersect(ctx, dm, far, mode=bzr.ACCEL_NONE)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    assert (a.view(np.uint32)[11] == 4).mean() > 0.05
     # random rays from everywhere around the cfg2 lens, incl. axis-parallel directions and far origins
     rng = np.random.default_rng(21)
     n = 200000
