@@ -48,6 +48,8 @@ def parse():
     p.add_argument("--side", type=int, default=0, help="override rays per image side (per rank)")
     p.add_argument("--gather", default="step", choices=["step", "none"])
     p.add_argument("--accel", default="bvh", choices=["bvh", "none"], help="none = brute-force scan (A/B)")
+    p.add_argument("--mode", default="parity", choices=["parity", "fast"],
+                   help="fast = BZR_MODE_FAST Newton stage (contracted FMA, approximate div/sqrt; not bit-exact)")
     p.add_argument("--cpu-baseline", default="on", choices=["on", "off"])
     p.add_argument("--cpu-sample-stride", type=int, default=2, help="oracle sample: every k-th row and column")
     return p.parse_args()
@@ -114,6 +116,8 @@ def main():
     torch.cuda.set_stream(stream)
     ctx.use_torch_stream(stream)
     mode = bzr_amd.ACCEL_NONE if a.accel == "none" else bzr_amd.MODE_PARITY
+    if a.mode == "fast":
+        mode |= bzr_amd.MODE_FAST
 
     _, _, rays_np = frame.rank_rays(cfg, rank, world, side, side * world)
     n = rays_np.shape[1]
@@ -265,7 +269,8 @@ def main():
                 "parallelism": f"image tiles x{world}" + (", RCCL gather of every frame to rank 0 (overlapped with the next frame)"
                                                           if world > 1 and a.gather == "step" else ""),
                 "scan": "BVH-culled (bit-identical to brute force)" if a.accel == "bvh" else "brute force",
-                "numerics": "parity: bit-identical to the CPU oracle",
+                "numerics": "parity: bit-identical to the CPU oracle" if a.mode == "parity" else
+                            "fast: exact planar gate, Newton stage with FMA + approximate div/sqrt (SURVEY 8c fast gates)",
                 "preprocess_s": round(prep_s, 3),
                 "upload_and_bvh_s": round(upload_s, 3),
             },

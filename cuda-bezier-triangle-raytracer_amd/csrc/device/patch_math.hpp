@@ -1,9 +1,11 @@
 // patch_math.hpp -- device arithmetic of the hot path, one ray per lane.
 //
-// Every function evaluates in IEEE binary32 with the operation order of the
-// reference (Eigen 3.3 fixed-size semantics, see include/bzr/bzr.hpp) and must
-// be compiled with -ffp-contract=off: the results are then bit-identical to
-// the CPU oracle (oracle/bzr_oracle.c), which tests/test_gpu_parity.py checks.
+// The exact:: arithmetic (patch_math_body.inc) evaluates in IEEE binary32 with the
+// operation order of the reference (Eigen 3.3 fixed-size semantics, see
+// include/bzr/bzr.hpp) and must be compiled with -ffp-contract=off: the results are
+// then bit-identical to the CPU oracle (oracle/bzr_oracle.c), which
+// tests/test_gpu_parity.py checks.  fast:: is the same text with contraction and
+// approximate div/sqrt, used after the (always exact) planar gate in BZR_MODE_FAST.
 //   plane_ray        reference/3dGeomUtil.h:279-296 (+ deviations D1/D2)
 //   interpolate      reference/bezierTriangle.cpp:105-121
 //   surface_normal   reference/bezierTriangle.cpp:197-233
@@ -15,33 +17,10 @@
 
 namespace bzr_dev {
 
-// Correctly rounded binary32 division and square root.  HIP compiles `/` and
-// __builtin_sqrtf correctly rounded by default (-fhip-fp32-correctly-rounded-divide-sqrt);
-// note __fsqrt_rn is NOT: it maps to the approximate __ocml_native_sqrt_f32 in ROCm 7.2.
-__device__ __forceinline__ float div_rn(float a, float b) { return a / b; }
-__device__ __forceinline__ float sqrt_rn(float a) { return __builtin_sqrtf(a); }
-
 struct f3 {
   float x, y, z;
 };
 __device__ __forceinline__ f3 mk(float x, float y, float z) { return f3{x, y, z}; }
-__device__ __forceinline__ f3 add(f3 a, f3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
-__device__ __forceinline__ f3 sub(f3 a, f3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
-__device__ __forceinline__ f3 scale(f3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
-__device__ __forceinline__ float dot(f3 a, f3 b) { return a.x * b.x + (a.y * b.y + a.z * b.z); }
-__device__ __forceinline__ f3 cross(f3 a, f3 b) {
-  return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
-}
-__device__ __forceinline__ f3 normalized(f3 a) {
-  float z = dot(a, a);
-  if (z > 0.0f) {
-    float s = sqrt_rn(z);
-    return mk(div_rn(a.x, s), div_rn(a.y, s), div_rn(a.z, s));
-  }
-  return a;
-}
-__device__ __forceinline__ float norm(f3 a) { return sqrt_rn(dot(a, a)); }
-
 // Patch record = the reference's BezierTriangle, 66 words (include/bzr.h bzr_patch).
 namespace rec {
 constexpr int kUnder = 0;     // n.xyz, c
@@ -124,66 +103,6 @@ __device__ __forceinline__ PatchView<const const_float *> uniform_patch(const fl
   return PatchView<const const_float *>{(const const_float *)(uintptr_t)(base + (size_t)rec::kWords * index)};
 }
 
-template <typename P>
-__device__ __forceinline__ f3 matvec(const P &p, f3 v) {  // Eigen row redux over the col-major M
-  return mk(p.m(0) * v.x + (p.m(3) * v.y + p.m(6) * v.z), p.m(1) * v.x + (p.m(4) * v.y + p.m(7) * v.z),
-            p.m(2) * v.x + (p.m(5) * v.y + p.m(8) * v.z));
-}
-
-// Plane::intersect(start, dir) with D1 (point for any t) and D2 (point = start when |cos| < eps)
-__device__ __forceinline__ bool plane_ray(f3 n, float c, f3 start, f3 dir, f3 &point, float &cs, float &t) {
-  cs = dot(dir, n);
-  if (fabsf(cs) >= 0.00001f) {
-    t = div_rn(c - dot(n, start), cs);
-    point = add(start, scale(dir, t));
-    return t > 0.0f;
-  }
-  t = 0.0f;
-  point = start;
-  return false;
-}
-
-__device__ __forceinline__ float plane_distance(f3 n, float c, f3 p) { return dot(p, n) - c; }
-__device__ __forceinline__ f3 plane_project(f3 n, float c, f3 p) { return sub(p, scale(n, dot(p, n) - c)); }
-
-template <typename P>
-__device__ __forceinline__ f3 interpolate(const P &p, f3 b) {
-  float q0 = b.x * b.x, q1 = b.y * b.y, q2 = b.z * b.z;
-#define c(k) p.cp(k)
-#define BZR_IP(F)                                                                                      \
-  (((((c(0).F * b.x) * q0 + (c(1).F * b.y) * q1) + (c(2).F * b.z) * q2) +                             \
-    3.0f * ((((((c(3).F * b.y) * q0 + (c(4).F * b.x) * q1) + (c(5).F * b.z) * q1) + (c(6).F * b.y) * q2) + \
-             (c(7).F * b.x) * q2) +                                                                    \
-            (c(8).F * b.z) * q0)) +                                                                    \
-   (((c(9).F * b.x) * b.y) * b.z) * 6.0f)
-  return mk(BZR_IP(x), BZR_IP(y), BZR_IP(z));
-#undef BZR_IP
-#undef c
-}
-
-template <typename P>
-__device__ __forceinline__ f3 surface_normal(const P &p, f3 b) {
-  float q0 = b.x * b.x, q1 = b.y * b.y, q2 = b.z * b.z;
-#define c(k) p.cp(k)
-  // control point slots: 300=0 030=1 003=2 210=3 120=4 021=5 012=6 102=7 201=8 111=9
-#define BZR_K0(F) (((c(0).F * q0 + c(7).F * q2) + c(4).F * q1) + 2.0f * (((c(8).F * b.x) * b.z + (c(3).F * b.x) * b.y) + (c(9).F * b.z) * b.y))
-#define BZR_K1(F) (((c(1).F * q1 + c(6).F * q2) + c(3).F * q0) + 2.0f * (((c(9).F * b.x) * b.z + (c(4).F * b.x) * b.y) + (c(5).F * b.y) * b.z))
-#define BZR_K2(F) (((c(2).F * q2 + c(8).F * q0) + c(5).F * q1) + 2.0f * (((c(7).F * b.x) * b.z + (c(6).F * b.y) * b.z) + (c(9).F * b.x) * b.y))
-  f3 k0 = mk(BZR_K0(x), BZR_K0(y), BZR_K0(z));
-  f3 k1 = mk(BZR_K1(x), BZR_K1(y), BZR_K1(z));
-  f3 k2 = mk(BZR_K2(x), BZR_K2(y), BZR_K2(z));
-#undef BZR_K0
-#undef BZR_K1
-#undef BZR_K2
-#undef c
-  const f3 da = p.da(), db = p.db();
-  f3 ca = mk((da.x * k0.x + da.y * k1.x) + da.z * k2.x, (da.x * k0.y + da.y * k1.y) + da.z * k2.y,
-             (da.x * k0.z + da.y * k1.z) + da.z * k2.z);
-  f3 cb = mk((db.x * k0.x + db.y * k1.x) + db.z * k2.x, (db.x * k0.y + db.y * k1.y) + db.z * k2.y,
-             (db.x * k0.z + db.y * k1.z) + db.z * k2.z);
-  return normalized(cross(ca, cb));
-}
-
 struct Hit {
   float t;
   f3 point;
@@ -198,10 +117,41 @@ struct Hit {
 #endif
 constexpr uint32_t kFollow2 = 2u, kNone = 3u, kIntersect = 4u;
 
+// Correctly rounded binary32 division and square root.  HIP compiles `/` and
+// __builtin_sqrtf correctly rounded by default (-fhip-fp32-correctly-rounded-divide-sqrt);
+// note __fsqrt_rn is NOT: it maps to the approximate __ocml_native_sqrt_f32 in ROCm 7.2.
+namespace exact {
+__device__ __forceinline__ float div_rn(float a, float b) { return a / b; }
+__device__ __forceinline__ float sqrt_rn(float a) { return __builtin_sqrtf(a); }
+__device__ __forceinline__ f3 unit(f3 a, float z) {  // Eigen normalized(): a / sqrt(z), three divisions
+  float s = sqrt_rn(z);
+  return mk(div_rn(a.x, s), div_rn(a.y, s), div_rn(a.z, s));
+}
+#include "patch_math_body.inc"
+}  // namespace exact
+
+// BZR_MODE_FAST: contracted FMA, v_rcp_f32 / v_sqrt_f32 / v_rsq_f32 (about 1 ulp each).
+namespace fast {
+#pragma clang fp contract(fast)
+__device__ __forceinline__ float div_rn(float a, float b) { return a * __builtin_amdgcn_rcpf(b); }
+__device__ __forceinline__ float sqrt_rn(float a) { return __builtin_amdgcn_sqrtf(a); }
+__device__ __forceinline__ f3 unit(f3 a, float z) {
+  float r = __builtin_amdgcn_rsqf(z);
+  return mk(a.x * r, a.y * r, a.z * r);
+}
+#include "patch_math_body.inc"
+#pragma clang fp contract(off)
+}  // namespace fast
+
+// Everything outside the Newton stage evaluates exactly.  (No arithmetic function is declared in
+// bzr_dev itself, so argument-dependent lookup on f3 / Patch never mixes the two namespaces.)
+using namespace exact;
+
 // BezierTriangle::intersect (reference/bezierTriangle.cpp:123-195).  limitNone: 0 = cThis, 1 = cNone.
 // kGated: the caller has already evaluated the planar gate (:124-131) with this same arithmetic and
 // it passed (the culled pipeline's candidates), so its early returns are skipped -- same result bits.
-template <bool kGated = false, typename P>
+// kFast: the gate stays exact (same candidates as the reference), the rest runs in fast::.
+template <bool kGated = false, bool kFast = false, typename P>
 __device__ __forceinline__ Hit patch_intersect(const P &p, f3 s, f3 d, bool limitNone) {
   Hit h;
   h.t = 0.0f;
@@ -213,57 +163,15 @@ __device__ __forceinline__ Hit patch_intersect(const P &p, f3 s, f3 d, bool limi
   f3 ip;
   float ic, it;
   bool valid = plane_ray(p.n(), p.c(), s, d, ip, ic, it);
+  (void)valid;
   if (!kGated) {
     if (!(valid && fabsf(it) > -p.hin() && fabsf(it) > p.hout())) return h;
     f3 b0 = matvec(p, ip);
     if (!(limitNone || (b0.x >= 0.0f && b0.x <= 1.0f && b0.y >= 0.0f && b0.y <= 1.0f && b0.z >= 0.0f && b0.z <= 1.0f)))
       return h;
   }
-  float din = div_rn(p.hin(), ic), dout = div_rn(p.hout(), ic);
-  float closer = it + (ic > 0.0f ? din : dout);
-  float further = it + (ic > 0.0f ? dout : din);
-  // secant start between the two bounding heights
-  f3 por = add(s, scale(d, closer));
-  f3 b = matvec(p, plane_project(p.n(), p.c(), por));
-  f3 q = interpolate(p, b);
-  float diffc = fabsf(plane_distance(p.n(), p.c(), por)) - fabsf(plane_distance(p.n(), p.c(), q));
-  por = add(s, scale(d, further));
-  b = matvec(p, plane_project(p.n(), p.c(), por));
-  q = interpolate(p, b);
-  float difff = fabsf(plane_distance(p.n(), p.c(), por)) - fabsf(plane_distance(p.n(), p.c(), q));
-  float den = diffc - difff;
-  float middle = fabsf(den) < 0.000001f ? div_rn(closer + further, 2.0f)
-                                        : div_rn(diffc * further - difff * closer, den);
-  f3 pdir = p.n();
-  for (int i = 0; i < BZR_NEWTON_ITERS; ++i) {  // csRootSearchIterations
-    h.t = middle;
-    por = add(s, scale(d, middle));
-    f3 pp;
-    float pc, pt;
-    plane_ray(p.n(), p.c(), por, pdir, pp, pc, pt);
-    h.bary = matvec(p, pp);
-    h.normal = surface_normal(p, h.bary);
-    h.point = interpolate(p, h.bary);
-    pdir = normalized(sub(h.point, pp));
-    middle = div_rn(dot(sub(h.point, s), h.normal), dot(d, h.normal));
-  }
-  f3 rel = sub(h.point, s);
-  f3 perp = sub(rel, scale(d, dot(rel, d)));
-  if (norm(perp) > 0.01f || h.t < (further - closer) * 1.0f) {
-    h.what = kNone;
-    return h;
-  }
-  uint32_t out = plane_distance(p.dn(0), p.dc(0), h.point) < 0.0f ? 1u : 0u;
-  out |= plane_distance(p.dn(1), p.dc(1), h.point) < 0.0f ? 2u : 0u;
-  out |= plane_distance(p.dn(2), p.dc(2), h.point) < 0.0f ? 4u : 0u;
-  if (out == 1u) h.what = 0u;
-  else if (out == 2u) h.what = 1u;
-  else if (out == 4u) h.what = 2u;
-  else {
-    h.what = kIntersect;
-    h.cs = dot(d, h.normal);
-  }
-  return h;
+  if constexpr (kFast) return fast::newton_tail(p, s, d, ic, it);
+  else return newton_tail(p, s, d, ic, it);
 }
 
 }  // namespace bzr_dev

@@ -197,13 +197,14 @@ __device__ __forceinline__ bool planar_gate(float4 q0, float4 q1, float4 q2, flo
 
 // One iteration of the reference loop body: patch b with cThis, and on a follow-side result its
 // named neighbour with cNone (reference/bezierMesh.cpp:212-216).  `src` gets the patch that hit.
+template <bool kFast = false>
 __device__ __forceinline__ Hit evaluate_patch(const MeshView &m, uint32_t b, f3 s, f3 d, uint32_t &src) {
   uint32_t idx = b;
   bool limitNone = false;
   Hit h;
   for (int pass = 0; pass < 2; ++pass) {
     Patch p = load_patch(m.full + (size_t)rec::kWords * idx);
-    h = patch_intersect(p, s, d, limitNone);
+    h = patch_intersect<false, kFast>(p, s, d, limitNone);
     if (pass == 0 && h.what <= kFollow2) {
       idx = __float_as_uint(m.full[(size_t)rec::kWords * idx + rec::kNeigh + h.what]);
       limitNone = true;
@@ -535,6 +536,7 @@ __device__ __forceinline__ void flush_follow(uint32_t *buf, uint32_t &nf, uint32
 // records while it computes the current one.  A chunk holds few distinct patches (buckets are
 // contiguous); each is processed with its record in scalar registers, `full` being a __restrict__
 // constant-address-space read.
+template <bool kFast>
 __global__ __launch_bounds__(kBlock) void k_newton(const float *__restrict__ full, const uint32_t *__restrict__ total,
                                                    const float4 *__restrict__ pairs, float *__restrict__ slot,
                                                    uint32_t cap, unsigned long long *__restrict__ key,
@@ -586,7 +588,7 @@ __global__ __launch_bounds__(kBlock) void k_newton(const float *__restrict__ ful
       if (todo && b == b0) {
         todo = false;
         // every pair passed this patch's planar gate in k_traverse (same arithmetic, same record values)
-        const Hit h = patch_intersect<BZR_NEWTON_GATED != 0>(pa, s, d, false);
+        const Hit h = patch_intersect<BZR_NEWTON_GATED != 0, kFast>(pa, s, d, false);
         if (h.what == kIntersect) record(slot, cap, p, h, b0, &key[ray]);
         is_fol = h.what <= kFollow2;
         fol_entry = p | (h.what << 30);
@@ -605,6 +607,7 @@ __global__ __launch_bounds__(kBlock) void k_newton(const float *__restrict__ ful
 
 // The chunks k_newton handed over (more than kLaneThreshold distinct patches): every lane runs its own
 // pair with its own patch record in VGPRs, so a fragmented chunk costs one pass instead of one per patch.
+template <bool kFast>
 __global__ __launch_bounds__(kBlock) void k_newton_lane(const float *__restrict__ full, const uint32_t *__restrict__ total,
                                                         const float4 *__restrict__ pairs, float *__restrict__ slot,
                                                         uint32_t cap, unsigned long long *__restrict__ key,
@@ -622,7 +625,7 @@ __global__ __launch_bounds__(kBlock) void k_newton_lane(const float *__restrict_
       const float4 a = pairs[p], e = pairs[(size_t)cap + p];
       const uint32_t b = __float_as_uint(e.w);
       const Patch pa = load_patch(full + (size_t)rec::kWords * b);
-      const Hit h = patch_intersect<BZR_NEWTON_GATED != 0>(pa, mk(a.x, a.y, a.z), mk(e.x, e.y, e.z), false);
+      const Hit h = patch_intersect<BZR_NEWTON_GATED != 0, kFast>(pa, mk(a.x, a.y, a.z), mk(e.x, e.y, e.z), false);
       if (h.what == kIntersect) record(slot, cap, p, h, b, &key[__float_as_uint(a.w)]);
       is_fol = h.what <= kFollow2;
       fol_entry = p | (h.what << 30);
@@ -637,6 +640,7 @@ __global__ __launch_bounds__(kBlock) void k_newton_lane(const float *__restrict_
   }
 }
 
+template <bool kFast>
 __global__ __launch_bounds__(kBlock) void k_follow(MeshView m, const float *__restrict__ rays, uint32_t ld,
                                                    uint32_t off, Work w) {
   const uint32_t F = __builtin_amdgcn_readfirstlane(w.ctr[0]);
@@ -646,12 +650,12 @@ __global__ __launch_bounds__(kBlock) void k_follow(MeshView m, const float *__re
     const f3 s = mk(a.x, a.y, a.z), d = mk(e.x, e.y, e.z);
     const uint32_t nbr = __float_as_uint(m.full[(size_t)rec::kWords * __float_as_uint(e.w) + rec::kNeigh + what]);
     Patch pa = load_patch(m.full + (size_t)rec::kWords * nbr);
-    Hit h = patch_intersect(pa, s, d, true);
+    Hit h = patch_intersect<false, kFast>(pa, s, d, true);
     if (h.what == kIntersect) record(w.slot, w.cap, p, h, nbr, &w.key[__float_as_uint(a.w)]);
   }
 }
 
-template <int kMode>
+template <int kMode, bool kFast>
 __global__ __launch_bounds__(kBlock) void k_finish(MeshView m, const float *rays, uint32_t ld, uint32_t off, uint32_t n,
                                                    Work w, Out o) {
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
@@ -664,7 +668,7 @@ __global__ __launch_bounds__(kBlock) void k_finish(MeshView m, const float *rays
   uint32_t patch = 0xFFFFFFFFu;
   const unsigned long long k = w.key[i];
   if (w.count[i] > kMaxCand) {  // overflow ray: k_overflow left (t order, scanned patch) -- evaluate it again
-    if (k != ~0ull) h = evaluate_patch(m, static_cast<uint32_t>(k), s, d, patch);
+    if (k != ~0ull) h = evaluate_patch<kFast>(m, static_cast<uint32_t>(k), s, d, patch);
   } else if (k != ~0ull) {
     const uint32_t p = static_cast<uint32_t>(k);
 
@@ -698,6 +702,7 @@ __device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v)
   return v;
 }
 
+template <bool kFast>
 __global__ __launch_bounds__(kBlock) void k_overflow(MeshView m, const float *rays, uint32_t ld, uint32_t off, Work w) {
   const uint32_t V = __builtin_amdgcn_readfirstlane(w.ctr[1]);
   const uint32_t S = (m.n + kOvfSlice - 1) / kOvfSlice;
@@ -713,7 +718,7 @@ __global__ __launch_bounds__(kBlock) void k_overflow(MeshView m, const float *ra
       const float4 *qq = m.planar + 4u * b;
       if (!planar_gate(qq[0], qq[1], qq[2], qq[3], s, d)) continue;
       uint32_t src;
-      Hit h = evaluate_patch(m, b, s, d, src);
+      Hit h = evaluate_patch<kFast>(m, b, s, d, src);
       if (h.what == kIntersect && h.t < best_t) {
         best_t = h.t;
         best_b = b;
@@ -799,6 +804,7 @@ __global__ __launch_bounds__(kBlock) void k_chain_scan(LensSet lenses, const flo
   if (out_segments) out_segments[i] = seg;
 }
 
+template <bool kFast>
 __global__ __launch_bounds__(kBlock) void k_patch(MeshView m, const uint32_t *__restrict__ idx,
                                                   const uint32_t *__restrict__ limit, const float *__restrict__ rays,
                                                   uint32_t n, float *__restrict__ hits) {
@@ -810,7 +816,7 @@ __global__ __launch_bounds__(kBlock) void k_patch(MeshView m, const uint32_t *__
   Hit h;
   if (pi < m.n) {
     Patch p = load_patch(m.full + (size_t)rec::kWords * pi);
-    h = patch_intersect(p, s, d, limit[i] != 0u);
+    h = patch_intersect<false, kFast>(p, s, d, limit[i] != 0u);
   } else {
     h = no_hit();
     h.t = 0.0f;
@@ -865,6 +871,13 @@ bzr_status check_ctx_mesh(bzr_ctx *ctx, const bzr_mesh *mesh) {
 }
 
 bool use_scan(uint32_t flags) { return (flags & BZR_ACCEL_NONE) != 0; }
+bool use_fast(uint32_t flags) { return (flags & BZR_MODE_FAST) != 0; }
+// BZR_MODE_FAST runs on the culled pipeline's kernels only; the brute-force scan is the parity reference.
+bzr_status check_flags(uint32_t flags) {
+  if (use_fast(flags) && use_scan(flags))
+    return set_error(BZR_ERR_INVALID_ARGUMENT, "BZR_MODE_FAST needs the culled path (drop BZR_ACCEL_NONE)");
+  return BZR_OK;
+}
 
 hipEvent_t take_event(bzr_ctx *ctx) {
   if (!ctx->spare.empty()) {
@@ -970,7 +983,7 @@ constexpr uint32_t kChunk = 1u << 20;
 uint32_t chunk_for(uint32_t n) { return n < kChunk ? n : kChunk; }
 
 // One BezierMesh::intersect per ray of rays [off, off + n) (+ refraction, per kMode).
-template <int kMode>
+template <int kMode, bool kFast>
 bzr_status run_culled(bzr_ctx *ctx, const MeshView &mv, const float *rays, uint32_t ld, uint32_t off, uint32_t n,
                       const uint32_t *alive, const Out &o, Work &w) {
   const uint32_t nb = mv.n;
@@ -985,23 +998,30 @@ bzr_status run_culled(bzr_ctx *ctx, const MeshView &mv, const float *rays, uint3
   }
   // persistent grid: the resident capacity of the device, never more than the worst-case chunk count
   const uint32_t gn = std::min<uint32_t>(std::max<uint32_t>((kMaxCand * n + kBlock - 1) / kBlock, 1u),
-                                         resident_blocks(ctx, k_newton));
-  launch(ctx, BZR_KERNEL_NEWTON, k_newton, dim3(gn), mv.full, w.offs + hn, w.pairs, w.slot, w.cap, w.key, w.fol,
+                                         resident_blocks(ctx, k_newton<kFast>));
+  launch(ctx, BZR_KERNEL_NEWTON, k_newton<kFast>, dim3(gn), mv.full, w.offs + hn, w.pairs, w.slot, w.cap, w.key, w.fol,
          w.ctr, w.lanes, w.ctr + 3);
-  launch(ctx, BZR_KERNEL_NEWTON_LANE, k_newton_lane, dim3(std::min<uint32_t>(std::max<uint32_t>(n / 1024u, 1u), 1024u)),
+  launch(ctx, BZR_KERNEL_NEWTON_LANE, k_newton_lane<kFast>, dim3(std::min<uint32_t>(std::max<uint32_t>(n / 1024u, 1u), 1024u)),
          mv.full, w.offs + hn, w.pairs, w.slot, w.cap, w.key, w.fol, w.ctr, w.lanes, w.ctr + 3);
-  launch(ctx, BZR_KERNEL_FOLLOW, k_follow, dim3(std::min<uint32_t>(grid_for(n / 8 + 1), 1024u)), mv, rays, ld, off,
+  launch(ctx, BZR_KERNEL_FOLLOW, k_follow<kFast>, dim3(std::min<uint32_t>(grid_for(n / 8 + 1), 1024u)), mv, rays, ld, off,
          w);
   {  // overflow rays' keys are untouched by the Newton stage (their lists are empty)
     const uint32_t items = n * ((nb + kOvfSlice - 1) / kOvfSlice);
-    launch(ctx, BZR_KERNEL_OVERFLOW, k_overflow, dim3(std::max<uint32_t>(std::min<uint32_t>(items, BZR_OVERFLOW_BLOCKS), 1u)),
+    launch(ctx, BZR_KERNEL_OVERFLOW, k_overflow<kFast>, dim3(std::max<uint32_t>(std::min<uint32_t>(items, BZR_OVERFLOW_BLOCKS), 1u)),
            mv, rays, ld, off, w);
   }
-  launch(ctx, BZR_KERNEL_FINISH, k_finish<kMode>, dim3(grid_for(n)), mv, rays, ld, off, n, w, o);
+  launch(ctx, BZR_KERNEL_FINISH, k_finish<kMode, kFast>, dim3(grid_for(n)), mv, rays, ld, off, n, w, o);
   if (ctx->counting && ctx->counters)
     hipLaunchKernelGGL(k_count, dim3(1), dim3(64), 0, ctx->stream, w, nb, ctx->counters);
   BZR_HIP(hipGetLastError());
   return BZR_OK;
+}
+
+template <int kMode>
+bzr_status run_segment(bool fast, bzr_ctx *ctx, const MeshView &mv, const float *rays, uint32_t ld, uint32_t off,
+                       uint32_t n, const uint32_t *alive, const Out &o, Work &w) {
+  return fast ? run_culled<kMode, true>(ctx, mv, rays, ld, off, n, alive, o, w)
+              : run_culled<kMode, false>(ctx, mv, rays, ld, off, n, alive, o, w);
 }
 
 }  // namespace
@@ -1215,6 +1235,7 @@ extern "C" bzr_status bzr_mesh_size(const bzr_mesh *mesh, uint32_t *n) {
 extern "C" bzr_status bzr_intersect(bzr_ctx *ctx, const bzr_mesh *mesh, const float *rays, uint32_t n, float *hits,
                                     uint32_t flags) {
   if (bzr_status s = check_ctx_mesh(ctx, mesh)) return s;
+  if (bzr_status s = check_flags(flags)) return s;
   if (n == 0) return BZR_OK;
   if (!rays || !hits) return set_error(BZR_ERR_INVALID_ARGUMENT, "null buffer");
   DeviceGuard g(ctx->device);
@@ -1240,7 +1261,7 @@ extern "C" bzr_status bzr_intersect(bzr_ctx *ctx, const bzr_mesh *mesh, const fl
     Out o{};
     o.hits = d_hits;
     for (uint32_t off = 0; off < n; off += ch)
-      if (bzr_status s = run_culled<kModeHits>(ctx, mv, d_rays, n, off, std::min(ch, n - off), nullptr, o, w))
+      if (bzr_status s = run_segment<kModeHits>(use_fast(flags), ctx, mv, d_rays, n, off, std::min(ch, n - off), nullptr, o, w))
         return s;
   }
   BZR_HIP(hipGetLastError());
@@ -1254,6 +1275,7 @@ extern "C" bzr_status bzr_intersect(bzr_ctx *ctx, const bzr_mesh *mesh, const fl
 extern "C" bzr_status bzr_patch_intersect(bzr_ctx *ctx, const bzr_mesh *mesh, const uint32_t *idx, const uint32_t *limit,
                                           const float *rays, uint32_t n, float *hits, uint32_t flags) {
   if (bzr_status s = check_ctx_mesh(ctx, mesh)) return s;
+  if (bzr_status s = check_flags(flags)) return s;
   if (n == 0) return BZR_OK;
   if (!idx || !limit || !rays || !hits) return set_error(BZR_ERR_INVALID_ARGUMENT, "null buffer");
   DeviceGuard g(ctx->device);
@@ -1276,7 +1298,8 @@ extern "C" bzr_status bzr_patch_intersect(bzr_ctx *ctx, const bzr_mesh *mesh, co
     d_lim = b;
     d_rays = r;
   }
-  launch(ctx, BZR_KERNEL_PATCH, k_patch, dim3(grid_for(n)), view_of(mesh), d_idx, d_lim, d_rays, n,
+  auto *kp = use_fast(flags) ? &k_patch<true> : &k_patch<false>;
+  launch(ctx, BZR_KERNEL_PATCH, kp, dim3(grid_for(n)), view_of(mesh), d_idx, d_lim, d_rays, n,
                      d_hits);
   BZR_HIP(hipGetLastError());
   if (host) {
@@ -1290,6 +1313,7 @@ extern "C" bzr_status bzr_refract(bzr_ctx *ctx, const bzr_mesh *mesh, float ri, 
                                   uint32_t expected_all, uint32_t n, float *out_rays, uint32_t *out_status,
                                   uint32_t flags) {
   if (bzr_status s = check_ctx_mesh(ctx, mesh)) return s;
+  if (bzr_status s = check_flags(flags)) return s;
   if (n == 0) return BZR_OK;
   if (!rays || !out_rays || !out_status) return set_error(BZR_ERR_INVALID_ARGUMENT, "null buffer");
   DeviceGuard g(ctx->device);
@@ -1326,7 +1350,7 @@ extern "C" bzr_status bzr_refract(bzr_ctx *ctx, const bzr_mesh *mesh, float ri, 
     o.status = d_st;
     o.ri = ri;
     for (uint32_t off = 0; off < n; off += ch)
-      if (bzr_status s = run_culled<kModeRefract>(ctx, mv, d_rays, n, off, std::min(ch, n - off), nullptr, o, w))
+      if (bzr_status s = run_segment<kModeRefract>(use_fast(flags), ctx, mv, d_rays, n, off, std::min(ch, n - off), nullptr, o, w))
         return s;
   }
   BZR_HIP(hipGetLastError());
@@ -1344,6 +1368,7 @@ extern "C" bzr_status bzr_trace_chain(bzr_ctx *ctx, const bzr_mesh *const *lense
   if (!ctx) return set_error(BZR_ERR_INVALID_ARGUMENT, "null context");
   if (nlens == 0 || nlens > kMaxLenses) return set_error(BZR_ERR_INVALID_ARGUMENT, "nlens must be 1..8");
   if (!lenses || !ri) return set_error(BZR_ERR_INVALID_ARGUMENT, "null lens list");
+  if (bzr_status s = check_flags(flags)) return s;
   LensSet set{};
   set.count = nlens;
   for (uint32_t l = 0; l < nlens; ++l) {
@@ -1392,7 +1417,7 @@ extern "C" bzr_status bzr_trace_chain(bzr_ctx *ctx, const bzr_mesh *const *lense
           o.status = d_st;
           o.segments = d_seg;
           o.ri = set.lens[l].ri;
-          if (bzr_status s = run_culled<kModeStage>(ctx, set.lens[l], d_out, n, off, m, d_st, o, w)) return s;
+          if (bzr_status s = run_segment<kModeStage>(use_fast(flags), ctx, set.lens[l], d_out, n, off, m, d_st, o, w)) return s;
         }
       }
     }
@@ -1436,6 +1461,7 @@ __global__ __launch_bounds__(kBlock) void k_tessellate(const float *__restrict__
 extern "C" bzr_status bzr_mesh_interpolate(bzr_ctx *ctx, const bzr_mesh *mesh, int32_t divisor, float *out_xyz,
                                            uint32_t flags) {
   if (bzr_status s = check_ctx_mesh(ctx, mesh)) return s;
+  if (bzr_status s = check_flags(flags)) return s;
   if (divisor < 1 || divisor > 4096) return set_error(BZR_ERR_INVALID_ARGUMENT, "divisor must be 1..4096");
   const uint32_t K = static_cast<uint32_t>(divisor) * static_cast<uint32_t>(divisor);
   const uint64_t total = (uint64_t)K * mesh->n;
@@ -1607,6 +1633,7 @@ extern "C" bzr_status bzr_illuminate(bzr_ctx *ctx, const bzr_mesh *const *lenses
   if (bzr_status s = check_emitter(em)) return s;
   if (!tg->bins_u || !tg->bins_v || !(tg->size_u > 0.0f) || !(tg->size_v > 0.0f))
     return set_error(BZR_ERR_INVALID_ARGUMENT, "target bins and sizes must be positive");
+  if (bzr_status s = check_flags(flags)) return s;
   LensSet set{};
   set.count = nlens;
   uint32_t nb = 0;
@@ -1663,7 +1690,7 @@ extern "C" bzr_status bzr_illuminate(bzr_ctx *ctx, const bzr_mesh *const *lenses
         o.status = d_st;
         o.segments = d_seg;
         o.ri = set.lens[l].ri;
-        if (bzr_status s = run_culled<kModeStage>(ctx, set.lens[l], d_rays, B, 0, m, d_st, o, w)) return s;
+        if (bzr_status s = run_segment<kModeStage>(use_fast(flags), ctx, set.lens[l], d_rays, B, 0, m, d_st, o, w)) return s;
       }
     hipLaunchKernelGGL(k_land, dim3(grid_for(m)), dim3(kBlock), 0, ctx->stream, *tg, make_float4(pn.x, pn.y, pn.z, pc),
                        cell_u, cell_v, d_rays, B, m, d_st, d_hist, d_stats);

@@ -29,9 +29,14 @@
  *   - Pointer residency is selected per call by BZR_DEVICE_PTRS; host-pointer
  *     calls are synchronous, device-pointer calls are asynchronous on the
  *     context's stream until bzr_sync().
- *   - Numerics: IEEE binary32 with the reference's operation order and no
- *     contraction, bit-identical to the CPU oracle (BZR_MODE_PARITY, the only
- *     mode implemented; BZR_MODE_FAST is reserved).
+ *   - Numerics: BZR_MODE_PARITY (default) is IEEE binary32 with the
+ *     reference's operation order and no contraction, bit-identical to the CPU
+ *     oracle.  BZR_MODE_FAST keeps the planar gate exact (same candidate
+ *     patches as the reference) and runs the Newton stage with FMA contraction
+ *     and the hardware's approximate reciprocal / square root; it meets the
+ *     SURVEY 8c fast-mode gates (hit/miss >= 99.5 %, t within 1e-5 relative on
+ *     >= 99 % of same-patch hits) but is not bit-exact.  FAST needs the culled
+ *     path: FAST | BZR_ACCEL_NONE returns BZR_ERR_INVALID_ARGUMENT.
  *   - Scan strategy: by default each lens mesh carries a BVH over the regions
  *     where each patch's planar gate can pass, and only those patches reach
  *     the Newton stage -- the output bits are the brute-force scan's.
