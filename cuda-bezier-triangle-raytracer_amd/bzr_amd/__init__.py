@@ -66,6 +66,7 @@ _SIGS = {
     "bzr_patch_intersect": [_P, _P, _P, _P, _P, _U32, _P, _U32],
     "bzr_refract": [_P, _P, _F, _P, _P, _U32, _U32, _P, _P, _U32],
     "bzr_trace_chain": [_P, _P, _P, _U32, _P, _U32, _P, _P, _P, _U32],
+    "bzr_trace_tiled": [_P, _U32, _P, _P, _U32, _P, _U32, _U32, _P, _P, _P, _U32],
     "bzr_mesh_interpolate": [_P, _P, _I32, _P, _U32],
     "bzr_emit": [_P, _P, ctypes.c_uint64, _U32, _P, _P, _U32],
     "bzr_illuminate": [_P, _P, _P, _U32, _P, ctypes.c_uint64, _P, _P, _P, _U32],
@@ -320,6 +321,25 @@ def trace_chain(ctx: Context, lenses, ri, rays, out_rays=None, out_status=None, 
     o, s, g = _Buf(out_rays, np.float32, True), _Buf(out_status, np.uint32, True), _Buf(out_segments, np.uint32, True)
     _check(lib().bzr_trace_chain(ctx.handle, ctypes.cast(handles, _P), ctypes.cast(ris, _P), nl, r.ptr, n, o.ptr, s.ptr,
                                  g.ptr, _residency(r, o, s, g) | mode))
+    return out_rays, out_status, out_segments
+
+
+def trace_tiled(ctxs, lenses, ri, rays, tile_rays=4096, mode=MODE_PARITY):
+    """bzr_trace_tiled: the chain over several contexts (one per device) from one process.
+    `lenses[d]` is the list of DeviceMesh living on ctxs[d]; rays are host arrays [6, n], ordered
+    tile-major.  -> (rays [6, n], status [n], segments [n]) in input order."""
+    nc, nl = len(ctxs), len(ri)
+    if len(lenses) != nc or any(len(ls) != nl for ls in lenses):
+        raise ValueError("lenses must hold one list of len(ri) meshes per context")
+    r = np.ascontiguousarray(rays, dtype=np.float32)
+    n = r.shape[1]
+    out_rays, out_status, out_segments = np.empty((6, n), np.float32), np.empty(n, np.uint32), np.empty(n, np.uint32)
+    cs = (_P * nc)(*[c.handle for c in ctxs])
+    hs = (_P * (nc * nl))(*[m.handle for ls in lenses for m in ls])
+    ris = (_F * nl)(*[float(x) for x in ri])
+    _check(lib().bzr_trace_tiled(ctypes.cast(cs, _P), nc, ctypes.cast(hs, _P), ctypes.cast(ris, _P), nl,
+                                 r.ctypes.data, n, tile_rays, out_rays.ctypes.data, out_status.ctypes.data,
+                                 out_segments.ctypes.data, mode))
     return out_rays, out_status, out_segments
 
 

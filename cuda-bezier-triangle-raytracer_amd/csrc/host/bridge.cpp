@@ -90,17 +90,39 @@ void traceChain(std::vector<BezierLens const *> const &lenses, Ray const *rays, 
   }
 }
 
+void traceChainTiled(std::vector<Context *> const &ctxs, std::vector<BezierLens const *> const &lenses,
+                     Ray const *rays, std::size_t n, Ray *outRays, RefractionResult *outStatus,
+                     uint32_t *outSegments, uint32_t tileRays) {
+  std::vector<bzr_ctx *> handles;
+  std::vector<bzr_mesh const *> meshes;  // [context][lens]
+  std::vector<float> ri;
+  for (auto const *l : lenses) ri.push_back(l->getRefractiveIndex());
+  for (Context *c : ctxs) {
+    handles.push_back(c->get());
+    for (auto const *l : lenses) meshes.push_back(l->getMesh().device(*c));
+  }
+  std::vector<float> in = raysToSoa(rays, n), out(6 * n);
+  std::vector<uint32_t> st(n);
+  check(bzr_trace_tiled(handles.data(), static_cast<uint32_t>(handles.size()), meshes.data(), ri.data(),
+                        static_cast<uint32_t>(lenses.size()), in.data(), static_cast<uint32_t>(n), tileRays, out.data(),
+                        st.data(), outSegments, BZR_HOST_PTRS));
+  for (std::size_t i = 0; i < n; ++i) {
+    outRays[i] = soaToRay(out, n, i);
+    outStatus[i] = static_cast<RefractionResult>(st[i]);
+  }
+}
+
 }  // namespace bzr
 
 bzr_mesh *BezierMesh::device(bzr::Context &ctx) const {
-  if (!mDevice || mDevice->owner != ctx.get()) {
-    auto dm = std::make_shared<bzr::DeviceMesh>();
-    dm->owner = ctx.get();
-    bzr::check(bzr_mesh_create(ctx.get(), mMesh.empty() ? nullptr : mMesh.data(), static_cast<uint32_t>(mMesh.size()),
-                               sizeof(BezierTriangle), &dm->mesh));
-    mDevice = dm;
-  }
-  return mDevice->mesh;
+  for (auto const &dm : mDevices)
+    if (dm->owner == ctx.get()) return dm->mesh;
+  auto dm = std::make_shared<bzr::DeviceMesh>();
+  dm->owner = ctx.get();
+  bzr::check(bzr_mesh_create(ctx.get(), mMesh.empty() ? nullptr : mMesh.data(), static_cast<uint32_t>(mMesh.size()),
+                             sizeof(BezierTriangle), &dm->mesh));
+  mDevices.push_back(dm);
+  return dm->mesh;
 }
 
 void BezierMesh::intersect(Ray const *rays, std::size_t n, BezierIntersection *out, uint32_t *patchIndex,

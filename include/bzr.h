@@ -171,6 +171,17 @@ bzr_status bzr_refract(bzr_ctx *ctx, const bzr_mesh *mesh, float refractive_inde
 bzr_status bzr_trace_chain(bzr_ctx *ctx, const bzr_mesh *const *lenses, const float *refractive_index,
                            uint32_t nlens, const float *rays_soa, uint32_t n, float *out_rays_soa,
                            uint32_t *out_status, uint32_t *out_segments, uint32_t flags);
+/* Multi-GPU refraction chain in ONE process (C/C++ hosts without torch.distributed):
+ * image-plane tiles are dealt round-robin to the contexts, one per device.  Tile k is the rays
+ * [k * tile_rays, (k + 1) * tile_rays) of the host SoA input (callers order rays tile-major, e.g.
+ * 64x64-pixel tiles of 4096 rays); context d traces tiles d, d + nctx, ... through its own copy of
+ * the lenses, lenses[d * nlens + l] living on ctxs[d]'s device, on its own host thread, and the
+ * results land in the host outputs in input order (same bits as one bzr_trace_chain over all rays).
+ * Host pointers only (BZR_DEVICE_PTRS is rejected); synchronous; the mode flags pass through. */
+bzr_status bzr_trace_tiled(bzr_ctx *const *ctxs, uint32_t nctx, const bzr_mesh *const *lenses,
+                           const float *refractive_index, uint32_t nlens, const float *rays_soa, uint32_t n,
+                           uint32_t tile_rays, float *out_rays_soa, uint32_t *out_status,
+                           uint32_t *out_segments, uint32_t flags);
 /* BezierMesh::interpolate(divisor) on the device (reference/bezierMesh.cpp:55-66): the tessellated
  * surface, divisor^2 sub-triangles of every patch, in the reference's order (sub-triangle outer,
  * patch inner).  out_xyz: divisor^2 * n_patches triangles x 3 vertices x 3 floats.  divisor >= 1.

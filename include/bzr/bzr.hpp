@@ -407,13 +407,13 @@ class BezierMesh final {
   // Batch interface (GPU).  patchIndex (optional) receives the index of the patch hit, ~0u on a miss.
   void intersect(Ray const *rays, std::size_t n, BezierIntersection *out, uint32_t *patchIndex = nullptr,
                  bzr::Context *ctx = nullptr) const;
-  // Device handle of this mesh on ctx (uploaded on first use and cached).
+  // Device handle of this mesh on ctx (uploaded on first use and cached per context).
   bzr_mesh *device(bzr::Context &ctx) const;
 
  private:
   std::vector<BezierTriangle> mMesh;
   Mesh::Face2neighbours mOriginalNeighbours;
-  mutable std::shared_ptr<bzr::DeviceMesh> mDevice;
+  mutable std::vector<std::shared_ptr<bzr::DeviceMesh>> mDevices;
 };
 
 // -------------------------------------------------------------- bezierLens.h
@@ -438,6 +438,11 @@ namespace bzr {
 // Whole refraction chain through `lenses` in one GPU launch (reference/test.cpp:376-401 semantics).
 void traceChain(std::vector<BezierLens const *> const &lenses, Ray const *rays, std::size_t n, Ray *outRays,
                 RefractionResult *outStatus, uint32_t *outSegments = nullptr, Context *ctx = nullptr);
+// The same chain over several devices from one process (bzr_trace_tiled): tiles of tileRays
+// consecutive rays dealt round-robin to `ctxs` (one per device, distinct), results in input order.
+void traceChainTiled(std::vector<Context *> const &ctxs, std::vector<BezierLens const *> const &lenses,
+                     Ray const *rays, std::size_t n, Ray *outRays, RefractionResult *outStatus,
+                     uint32_t *outSegments = nullptr, uint32_t tileRays = 4096);
 }  // namespace bzr
 
 static_assert(sizeof(BezierTriangle) == sizeof(bzr_patch), "BezierTriangle must match the 264-byte record");

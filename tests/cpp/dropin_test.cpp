@@ -192,6 +192,14 @@ static void hot_path(Mesh const &lensMesh) {
   int chainExits = 0;
   for (auto s : status) chainExits += s == RefractionResult::cOutside;
   CHECK(chainExits == exits);
+  // the same chain dealt over two contexts (two streams / host threads on device 0), tiles of 100 rays
+  bzr::Context c0(0), c1(0);
+  std::vector<Ray> outT(rays.size());
+  std::vector<RefractionResult> statusT(rays.size());
+  std::vector<uint32_t> segT(rays.size());
+  bzr::traceChainTiled({&c0, &c1}, {&lens}, rays.data(), rays.size(), outT.data(), statusT.data(), segT.data(), 100);
+  CHECK(statusT == status && segT == seg);
+  CHECK(std::memcmp(outT.data(), out.data(), out.size() * sizeof(Ray)) == 0);
   std::printf("hot path: %d hits, %d exits of %zu rays\n", hits, exits, rays.size());
 }
 

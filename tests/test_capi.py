@@ -55,6 +55,22 @@ def test_errors_are_status_codes(bzr):
         bzr.TriMesh().make_ellipsoid(4, 2).bezier_patches()
 
 
+def test_trace_tiled_validates_before_touching_a_device(bzr):
+    import ctypes
+    L = bzr.lib()
+    f = (ctypes.c_float * 1)(1.3)
+    assert L.bzr_trace_tiled(None, 0, None, f, 1, None, 0, 4096, None, None, None, 0) == 1
+    assert b"no contexts" in L.bzr_last_error()
+    fake = (ctypes.c_void_p * 2)(1, 1)  # the same context twice: rejected (one host thread per context)
+    assert L.bzr_trace_tiled(fake, 2, fake, f, 1, None, 0, 4096, None, None, None, 0) == 1
+    assert b"repeated context" in L.bzr_last_error()
+    one = (ctypes.c_void_p * 1)(1)
+    assert L.bzr_trace_tiled(one, 1, one, f, 1, None, 0, 0, None, None, None, 0) == 1
+    assert b"tile_rays" in L.bzr_last_error()
+    assert L.bzr_trace_tiled(one, 1, one, f, 1, None, 0, 64, None, None, None, bzr.DEVICE_PTRS) == 1
+    assert b"host pointers" in L.bzr_last_error()
+
+
 def test_patch_records_view_as_reference_struct(bzr):
     """The 66-word records reinterpret as the bzr_patch / BezierTriangle layout: neighbours are u32 indices
     into the patch array, the direction vector A is (1, 0, -1) (reference/bezierTriangle.cpp:83)."""
