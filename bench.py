@@ -80,6 +80,23 @@ def cpu_baseline(cfg, side, patches, ris, stride):
     }, cnt
 
 
+def pmc_traffic(kernel, workload, same_workload):
+    """HBM bytes per launch of `kernel` ("a+b" sums the parts) from the committed PMC profile of this
+    workload (profiles/pmc_traffic.json, written by scripts/prof_summary.py from rocprofv3 FETCH_SIZE x2
+    + WRITE_SIZE passes over bench.py).  PMC counters cannot be read from inside the timed process."""
+    path = REPO / "profiles" / "pmc_traffic.json"
+    if not same_workload or not path.exists():
+        return None, None
+    d = json.loads(path.read_text())
+    if d.get("workload") != workload:
+        return None, None
+    parts = kernel.split("+")
+    if not all(p in d["kernels"] for p in parts):
+        return None, None
+    total = sum(d["kernels"][p].get("read", 0.0) + d["kernels"][p].get("write", 0.0) for p in parts)
+    return round(total), f"{d['source']} ({d['method']})"
+
+
 def main():
     a = parse()
     import torch
@@ -247,6 +264,7 @@ def main():
         d = per_kernel[dom]
         achieved = d["alg_tflops"]
         alg_bytes = n * BYTES_PER_PRIMARY
+        traffic, traffic_src = pmc_traffic(dom, cfg.name, side == cfg.side and world == 1 and a.mode == "parity")
         line = {
             "metric": "Mrays/sec (primary+refracted) at 1/2/4/8 MI355X; % of HBM-read roofline",
             "value": round(value, 3),
@@ -282,7 +300,9 @@ def main():
                 "peak": VALU_PEAK_TFLOPS,
                 "unit": "TFLOP/s",
                 "frac": round(achieved / VALU_PEAK_TFLOPS, 4),
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_unit": "HBM bytes per launch",
+                "traffic_source": traffic_src,
                 "avg_launch_ms": d["avg_launch_ms"],
                 "work": d["work"],
                 "per_kernel": per_kernel,

@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
 """Summarise rocprofv3 output databases (kernel-trace stats + PMC counters) into a text file.
 
-usage: prof_summary.py <out.txt> [--trace DIR] [--pmc DIR ...] [--note TEXT]
+usage: prof_summary.py <out.txt> [--trace DIR] [--pmc DIR ...] [--note TEXT] [--traffic-json OUT --workload W]
+       prof_summary.py --from-txt SUMMARY.txt --traffic-json OUT --workload W
+--traffic-json writes the per-kernel HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE) that bench.py
+reports as roofline.traffic for the same workload.
 FETCH_SIZE is doubled for the byte estimate: on gfx950 it reports half the bytes of a wide
 coalesced read (MI355X_MICROARCH.md, HBM section); WRITE_SIZE is taken as is.
 """
@@ -22,11 +25,17 @@ def short(name, n=90):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("out")
+    ap.add_argument("out", nargs="?")
     ap.add_argument("--trace", default=None)
     ap.add_argument("--pmc", nargs="*", default=[])
     ap.add_argument("--note", default="")
+    ap.add_argument("--traffic-json", default=None)
+    ap.add_argument("--workload", default="cfg2")
+    ap.add_argument("--from-txt", default=None)
     a = ap.parse_args()
+    if a.from_txt:
+        write_traffic(open(a.from_txt).read().splitlines(), a.from_txt, a.traffic_json, a.workload)
+        return
     lines = []
     if a.note:
         lines += [a.note, ""]
@@ -65,6 +74,25 @@ def main():
             lines.append("")
     open(a.out, "w").write("\n".join(lines) + "\n")
     print("\n".join(lines))
+    if a.traffic_json:
+        write_traffic(lines, a.out, a.traffic_json, a.workload)
+
+
+def write_traffic(lines, source, out, workload):
+    """Per-kernel HBM bytes per launch from the summary's PMC lines -> JSON for bench.py."""
+    import json
+    import re
+    kern = {}
+    for ln in lines:
+        m = re.match(r"^(?:void )?(k_\w+)[<(].*(?:est\. HBM read|HBM write) ([0-9.]+) MB/launch", ln)
+        if not m:
+            continue
+        key = "read" if "HBM read" in ln else "write"
+        kern.setdefault(m.group(1), {})[key] = float(m.group(2)) * 1e6
+    json.dump({"workload": workload, "source": source, "unit": "bytes per launch",
+               "method": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950 correction) and WRITE_SIZE, separate passes",
+               "kernels": kern}, open(out, "w"), indent=1)
+    print(f"wrote {out}: {len(kern)} kernels")
 
 
 if __name__ == "__main__":
