@@ -7,6 +7,7 @@ cfg4: two cfg2 lenses, 4096^2 rays, refraction chain (BASELINE quotes it on 8 GP
 cfg5: 301056-patch ellipsoid, BezierMesh::intersect; 4096^2 of its 8192^2 grid (one quarter: the full
       grid is 8 GPUs' work, 2x one rank's share).
 Inputs resident in HBM; K timed repetitions after one warm-up; Mrays/s counts BezierMesh::intersect calls.
+usage: bench_configs.py [cfg3 cfg4 cfg5] [--fast]   (--fast: BZR_MODE_FAST)
 """
 import json
 import sys
@@ -24,7 +25,7 @@ import bzr_amd  # noqa: E402
 from bzr_amd.configs import CONFIGS, build_lens, grid_rays  # noqa: E402
 
 
-def run(name, side, reps):
+def run(name, side, reps, mode=bzr_amd.MODE_PARITY):
     cfg = CONFIGS[name]
     t0 = time.perf_counter()
     patches = [build_lens(bzr_amd.TriMesh, l).bezier_patches() for l in cfg.lenses]
@@ -43,13 +44,13 @@ def run(name, side, reps):
                    torch.empty(n, dtype=torch.int32, device="cuda"))
 
         def step():
-            bzr_amd.trace_chain(ctx, meshes, [l.ri for l in cfg.lenses], rays, o, s, g)
+            bzr_amd.trace_chain(ctx, meshes, [l.ri for l in cfg.lenses], rays, o, s, g, mode=mode)
     else:
         hits = torch.empty((13, n), device="cuda")
         g = None
 
         def step():
-            bzr_amd.intersect(ctx, meshes[0], rays, hits)
+            bzr_amd.intersect(ctx, meshes[0], rays, hits, mode=mode)
     step()
     torch.cuda.synchronize()
     segs = int(g.sum().item()) if g is not None else n
@@ -71,7 +72,7 @@ def run(name, side, reps):
     extra = {"kernels_ms": kern, "counters": cnt}
     if g is None:
         extra["hit_fraction"] = round(float((hits[11].view(torch.int32) == 4).float().mean().item()), 4)
-    print(json.dumps({"config": name, "rays_side": side, "patches": int(sum(len(p) for p in patches)),
+    print(json.dumps({"config": name, "mode": "fast" if mode & bzr_amd.MODE_FAST else "parity", "rays_side": side, "patches": int(sum(len(p) for p in patches)),
                       "segments_per_step": segs, "ms_per_step": round(dt * 1e3, 3),
                       "mrays_per_s": round(segs / dt / 1e6, 1), "preprocess_s": round(prep, 2),
                       "upload_bvh_s": round(upload, 2), **extra}), flush=True)
@@ -80,10 +81,12 @@ def run(name, side, reps):
 
 
 def main():
-    which = sys.argv[1:] or ["cfg3", "cfg4", "cfg5"]
+    args = sys.argv[1:]
+    mode = bzr_amd.MODE_FAST if "--fast" in args else bzr_amd.MODE_PARITY
+    which = [a for a in args if not a.startswith("--")] or ["cfg3", "cfg4", "cfg5"]
     plan = {"cfg3": (2048, 10), "cfg4": (4096, 5), "cfg5": (4096, 3)}
     for name in which:
-        run(name, *plan[name])
+        run(name, *plan[name], mode=mode)
 
 
 if __name__ == "__main__":
