@@ -62,10 +62,13 @@ struct bzr_mesh {
   uint32_t n;
   float4 *planar;   // 4 float4 per patch: n.xyz c | hin hout M00 M01 | M02 M10 M11 M12 | M20 M21 M22 0
   float *full;      // 66 words per patch (bzr_patch)
-  bzr_host::Bvh4Node *nodes;  // 4-wide BVH over the patches' gate-region boxes (bvh.cpp)
+  bzr_host::Bvh4Node *nodes;  // 4-wide BVH over the patches' gate-region boxes (bvh.cpp), far tier
   float4 *leaf;     // 4 float4 per BVH leaf slot: the planar record, patch index in the last word
+  bzr_host::Bvh4Node *nodes_near;  // the near tier's tree and leaf slots (bvh.hpp kTierNear)
+  float4 *leaf_near;
   uint32_t nnodes;
-  float s_max;
+  float s_max;      // far tier: origins beyond take the full scan
+  float s_near;     // near tier: waves whose rays all start within it walk the tighter tree
   float sphere[4];  // Ritter sphere over the gate-region boxes (bvh.cpp): the illumination pre-cull
 };
 
@@ -145,8 +148,11 @@ struct MeshView {
   const float *__restrict__ full;
   const bzr_host::Bvh4Node *__restrict__ nodes;
   const float4 *__restrict__ leaf;
+  const bzr_host::Bvh4Node *__restrict__ nodes_near;
+  const float4 *__restrict__ leaf_near;
   uint32_t n;
   float s_max;
+  float s_near;
   float ri;
 };
 struct LensSet {
@@ -402,6 +408,11 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
     cnt = kOverflow;
     active = false;
   }
+  // tree tier, wave-uniform: the near tree's tighter boxes hold when every active ray starts within s_near
+  const bool far_ray = active && !(fmaxf(fmaxf(fabsf(s.x), fabsf(s.y)), fabsf(s.z)) <= m.s_near);
+  const bool near_tier = !__any(far_ray);
+  const bzr_host::Bvh4Node *nodes = near_tier ? m.nodes_near : m.nodes;
+  const float4 *leaf = near_tier ? m.leaf_near : m.leaf;
   const f3 inv = mk(safe_inv(d.x), safe_inv(d.y), safe_inv(d.z));
   const f3 sinv = mk(s.x * inv.x, s.y * inv.y, s.z * inv.z);
   int sp = 0;
@@ -412,7 +423,7 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
   while (sp > 0) {
     const uint32_t node = __builtin_amdgcn_readfirstlane(stk[--sp]);
     // the whole 128-byte node in two 64-byte scalar loads and one wait (all words used unconditionally)
-    const cu32x16 *np = (const cu32x16 *)(uintptr_t)(m.nodes + node);
+    const cu32x16 *np = (const cu32x16 *)(uintptr_t)(nodes + node);
     const u32x16 na = np[0], nb = np[1];
     // words: lo.x[0..3] lo.y lo.z hi.x | hi.y hi.z child[0..3] pad
     bool hit[4];
@@ -428,7 +439,7 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
     for (int c = 0; c < 4; ++c) {
       if (!__any(hit[c])) continue;
       if (ch[c] & bzr_host::kLeafFlag) {
-        const u32x16 r = *((const cu32x16 *)(uintptr_t)m.leaf + (ch[c] & ~bzr_host::kLeafFlag));
+        const u32x16 r = *((const cu32x16 *)(uintptr_t)leaf + (ch[c] & ~bzr_host::kLeafFlag));
         const float4 q0 = make_float4(__uint_as_float(r[0]), __uint_as_float(r[1]), __uint_as_float(r[2]), __uint_as_float(r[3]));
         const float4 q1 = make_float4(__uint_as_float(r[4]), __uint_as_float(r[5]), __uint_as_float(r[6]), __uint_as_float(r[7]));
         const float4 q2 = make_float4(__uint_as_float(r[8]), __uint_as_float(r[9]), __uint_as_float(r[10]), __uint_as_float(r[11]));
@@ -837,7 +848,7 @@ struct DeviceGuard {
 };
 
 MeshView view_of(const bzr_mesh *m, float ri = 1.0f) {
-  return MeshView{m->planar, m->full, m->nodes, m->leaf, m->n, m->s_max, ri};
+  return MeshView{m->planar, m->full, m->nodes, m->leaf, m->nodes_near, m->leaf_near, m->n, m->s_max, m->s_near, ri};
 }
 unsigned grid_for(uint32_t n) { return (n + kBlock - 1) / kBlock; }
 size_t round256(size_t b) { return (b + 255) & ~size_t(255); }
@@ -1170,24 +1181,30 @@ extern "C" bzr_status bzr_mesh_create(bzr_ctx *ctx, const void *patches, uint32_
     planar[4 * i + 2] = make_float4(m[6], m[1], m[4], m[7]);
     planar[4 * i + 3] = make_float4(m[2], m[5], m[8], 0.0f);
   }
-  bzr_host::Bvh bvh;
+  bzr_host::Bvh bvh, bvh_near;
   try {
-    bvh = bzr_host::build_bvh(full.data(), n, rec::kWords);
+    bvh = bzr_host::build_bvh(full.data(), n, rec::kWords, bzr_host::kTierFar);
+    bvh_near = bzr_host::build_bvh(full.data(), n, rec::kWords, bzr_host::kTierNear);
   } catch (std::exception const &e) {
     return set_error(BZR_ERR_OUT_OF_MEMORY, std::string("BVH build: ") + e.what());
   }
-  std::vector<float4> leaf((size_t)n * 4);  // BVH slot order, patch index in the last word
-  for (uint32_t k = 0; k < n; ++k) {
-    uint32_t b = bvh.order[k];
-    for (int j = 0; j < 4; ++j) leaf[4 * k + j] = planar[4 * b + j];
-    std::memcpy(&leaf[4 * k + 3].w, &b, 4);
-  }
+  auto leaves = [&](bzr_host::Bvh const &t) {  // BVH slot order, patch index in the last word
+    std::vector<float4> leaf((size_t)n * 4);
+    for (uint32_t k = 0; k < n; ++k) {
+      uint32_t b = t.order[k];
+      for (int j = 0; j < 4; ++j) leaf[4 * k + j] = planar[4 * b + j];
+      std::memcpy(&leaf[4 * k + 3].w, &b, 4);
+    }
+    return leaf;
+  };
+  const std::vector<float4> leaf = leaves(bvh), leaf_near = leaves(bvh_near);
   bzr_mesh *mesh = new (std::nothrow) bzr_mesh();
   if (!mesh) return set_error(BZR_ERR_OUT_OF_MEMORY, "mesh allocation");
   mesh->device = ctx->device;
   mesh->n = n;
   mesh->nnodes = static_cast<uint32_t>(bvh.nodes4.size());
   mesh->s_max = bvh.s_max;
+  mesh->s_near = std::min(bvh_near.s_max, bvh.s_max);
   for (int k = 0; k < 4; ++k) mesh->sphere[k] = bvh.sphere[k];
   struct Up {
     void **dst;
@@ -1198,6 +1215,9 @@ extern "C" bzr_status bzr_mesh_create(bzr_ctx *ctx, const void *patches, uint32_
       {reinterpret_cast<void **>(&mesh->full), full.data(), full.size() * sizeof(float)},
       {reinterpret_cast<void **>(&mesh->nodes), bvh.nodes4.data(), bvh.nodes4.size() * sizeof(bzr_host::Bvh4Node)},
       {reinterpret_cast<void **>(&mesh->leaf), leaf.data(), leaf.size() * sizeof(float4)},
+      {reinterpret_cast<void **>(&mesh->nodes_near), bvh_near.nodes4.data(),
+       bvh_near.nodes4.size() * sizeof(bzr_host::Bvh4Node)},
+      {reinterpret_cast<void **>(&mesh->leaf_near), leaf_near.data(), leaf_near.size() * sizeof(float4)},
   };
   hipError_t e = hipSuccess;
   for (auto &u : ups) {
@@ -1222,6 +1242,8 @@ extern "C" bzr_status bzr_mesh_destroy(bzr_mesh *mesh) {
   (void)hipFree(mesh->full);
   (void)hipFree(mesh->nodes);
   (void)hipFree(mesh->leaf);
+  (void)hipFree(mesh->nodes_near);
+  (void)hipFree(mesh->leaf_near);
   delete mesh;
   return BZR_OK;
 }

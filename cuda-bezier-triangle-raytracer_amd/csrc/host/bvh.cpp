@@ -331,19 +331,19 @@ uint32_t collapse(std::vector<BvhNode> const &bin, uint32_t n2, std::vector<Bvh4
 
 }  // namespace
 
-Bvh build_bvh(const float *records, uint32_t n, uint32_t stride_words) {
+Bvh build_bvh(const float *records, uint32_t n, uint32_t stride_words, int tier) {
   Bvh out;
   std::vector<Box> box(n);
   Builder bld{box, std::vector<std::array<float, 3>>(n), out.order, out.nodes};
-  // ray origins up to s_max (100x the mesh's control-point extent, at least 1e3) use the culled
-  // path; farther origins are routed to the brute-force scan by the kernel.
+  // ray origins up to s_max use this tree (far tier: 100x the mesh's control-point extent, at least
+  // 1e3, farther origins are routed to the brute-force scan by the kernel; near tier: 8x, see bvh.hpp)
   double span = 0.0;
   for (uint32_t i = 0; i < n; ++i)
     for (int k = 0; k < 30; ++k) {
       double x = std::fabs(records[(size_t)i * stride_words + 19 + k]);
       if (std::isfinite(x)) span = std::max(span, x);
     }
-  out.s_max = static_cast<float>(std::max(1e3, 100.0 * span));
+  out.s_max = static_cast<float>(tier == kTierNear ? std::max(1.0, 8.0 * span) : std::max(1e3, 100.0 * span));
   out.extent = 0.0f;
   for (uint32_t i = 0; i < n; ++i) {
     box[i] = gate_region_box(records + (size_t)i * stride_words, out.s_max);
@@ -423,9 +423,11 @@ void ritter_sphere(std::vector<Box> const &box, float out[4]) {
 }  // namespace bzr_host
 
 // ---- debug / test entry point (include/bzr_debug.h) ----
-extern "C" int32_t bzr_debug_gate_boxes(const void *patches, uint32_t n, uint32_t stride, float *boxes, float *s_max) {
+extern "C" int32_t bzr_debug_gate_boxes_tier(const void *patches, uint32_t n, uint32_t stride, int32_t tier,
+                                             float *boxes, float *s_max) {
   if ((!patches && n) || (!boxes && n) || !s_max || stride % 4 || stride < 264) return 1;
-  bzr_host::Bvh bvh = bzr_host::build_bvh(static_cast<const float *>(patches), n, stride / 4);
+  if (tier != bzr_host::kTierFar && tier != bzr_host::kTierNear) return 1;
+  bzr_host::Bvh bvh = bzr_host::build_bvh(static_cast<const float *>(patches), n, stride / 4, tier);
   for (uint32_t k = 0; k < n; ++k) {
     uint32_t p = bvh.order[k];
     for (int a = 0; a < 3; ++a) {
@@ -435,6 +437,10 @@ extern "C" int32_t bzr_debug_gate_boxes(const void *patches, uint32_t n, uint32_
   }
   *s_max = bvh.s_max;
   return 0;
+}
+
+extern "C" int32_t bzr_debug_gate_boxes(const void *patches, uint32_t n, uint32_t stride, float *boxes, float *s_max) {
+  return bzr_debug_gate_boxes_tier(patches, n, stride, bzr_host::kTierFar, boxes, s_max);
 }
 
 namespace {
@@ -456,7 +462,8 @@ bool slab_h(const float lo[3], const float hi[3], const float s[3], const float 
 extern "C" int32_t bzr_debug_traverse(const void *patches, uint32_t n, uint32_t stride, const float *rays, uint32_t nr,
                                       uint8_t *hits, uint64_t stats[4]) {
   if ((!patches && n) || (!rays && nr) || !stats || stride % 4 || stride < 264) return 1;
-  bzr_host::Bvh bvh = bzr_host::build_bvh(static_cast<const float *>(patches), n, stride / 4);
+  bzr_host::Bvh far = bzr_host::build_bvh(static_cast<const float *>(patches), n, stride / 4, bzr_host::kTierFar);
+  bzr_host::Bvh near = bzr_host::build_bvh(static_cast<const float *>(patches), n, stride / 4, bzr_host::kTierNear);
   for (int k = 0; k < 4; ++k) stats[k] = 0;
   for (uint32_t w0 = 0; w0 < nr; w0 += 64) {
     uint32_t lanes = std::min<uint32_t>(64, nr - w0);
@@ -468,8 +475,12 @@ extern "C" int32_t bzr_debug_traverse(const void *patches, uint32_t n, uint32_t 
         s[l][k] = rays[(size_t)k * nr + r];
         inv[l][k] = safe_inv_h(rays[(size_t)(3 + k) * nr + r]);
       }
-      active[l] = std::fmax(std::fmax(std::fabs(s[l][0]), std::fabs(s[l][1])), std::fabs(s[l][2])) <= bvh.s_max;
+      active[l] = std::fmax(std::fmax(std::fabs(s[l][0]), std::fabs(s[l][1])), std::fabs(s[l][2])) <= far.s_max;
     }
+    bool all_near = true;  // the kernel's wave-uniform tier choice
+    for (uint32_t l = 0; l < lanes; ++l)
+      all_near &= !active[l] || std::fmax(std::fmax(std::fabs(s[l][0]), std::fabs(s[l][1])), std::fabs(s[l][2])) <= near.s_max;
+    bzr_host::Bvh const &bvh = all_near ? near : far;
     stats[3] += 1;
     if (!n) continue;
     std::vector<uint32_t> stack{0u};

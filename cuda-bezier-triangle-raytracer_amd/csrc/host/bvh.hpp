@@ -45,7 +45,14 @@ struct Bvh {
 
 void ritter_sphere(std::vector<Box> const &box, float out[4]);
 
+// Two trees per lens, built from the same patches for two origin radii (the gate-region boxes' rounding
+// slack grows with the radius the ray origins may have):
+//   kTierFar   s_max = max(1e3, 100 x span): every ray the culled path takes (farther -> full scan)
+//   kTierNear  s_max = max(1, 8 x span): tighter boxes, for waves whose rays all start within it
+//              (refracted segments start on the lens; primaries usually start near it)
+// span = the largest |control-point coordinate| of the mesh.
+constexpr int kTierFar = 0, kTierNear = 1;
 // records: n patch records of stride_words floats (bzr_patch layout, 66 words)
-Bvh build_bvh(const float *records, uint32_t n, uint32_t stride_words);
+Bvh build_bvh(const float *records, uint32_t n, uint32_t stride_words, int tier = kTierFar);
 
 }  // namespace bzr_host

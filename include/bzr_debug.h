@@ -10,9 +10,13 @@ extern "C" {
 /* The culling boxes the BVH is built from, by patch index: boxes[6*i] = lo.xyz, hi.xyz of the region
  * where patch i's planar gate can pass for ray origins with |s|_inf <= *s_max.  Returns 0 on success. */
 int32_t bzr_debug_gate_boxes(const void *patches, uint32_t n, uint32_t stride, float *boxes, float *s_max);
+/* The same for one BVH tier: 0 = far (as above), 1 = near (bvh.hpp kTierNear; tighter boxes, valid for
+ * origins |s|_inf <= *s_max, which is 8x the mesh's control-point span). */
+int32_t bzr_debug_gate_boxes_tier(const void *patches, uint32_t n, uint32_t stride, int32_t tier, float *boxes,
+                                  float *s_max);
 /* The bounding sphere bzr_illuminate culls with (Ritter over the gate boxes): centre xyz, radius. */
 int32_t bzr_debug_bounding_sphere(const void *patches, uint32_t n, uint32_t stride, float out[4]);
-/* Host replay of the device BVH walk (same 4-wide tree, same float slab test) over `nr` rays in SoA
+/* Host replay of the device BVH walk (same 4-wide trees and wave-uniform tier choice, same float slab test) over `nr` rays in SoA
  * [6, nr], grouped in waves of 64 consecutive rays.  hits (optional, nr x n bytes): hits[r*n + b] = 1
  * when ray r reaches patch b's leaf box -- a superset of the patches whose planar gate it passes.
  * stats[0] node visits (per wave), [1] leaf records fetched (per wave), [2] leaf-box hits (per ray),

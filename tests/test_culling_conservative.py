@@ -3,7 +3,8 @@
 the traversal kernel runs against that patch's gate-region box (csrc/host/bvh.cpp,
 csrc/device/trace.hip `slab`).  A pair that passes the gate but misses its box would silently change
 the result; this checks it on CPU for grazing, far, random and config rays -- including the
-ill-conditioned patches whose plane passes near the origin."""
+ill-conditioned patches whose plane passes near the origin.  Both BVH tiers are checked:
+the far tier (origins up to 100x the mesh span) and the near tier (tighter boxes, origins up to 8x)."""
 import ctypes
 
 import numpy as np
@@ -12,15 +13,18 @@ import pytest
 from bzr_amd.configs import CONFIGS, build_lens, grid_rays
 
 
-def gate_boxes(bzr, patches):
+TIERS = [0, 1]  # bvh.hpp kTierFar, kTierNear
+
+
+def gate_boxes(bzr, patches, tier=0):
     L = bzr.lib()
-    fn = L.bzr_debug_gate_boxes
-    fn.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
+    fn = L.bzr_debug_gate_boxes_tier
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p]
     fn.restype = ctypes.c_int32
     p = np.ascontiguousarray(patches, np.float32)
     boxes = np.zeros((len(p), 6), np.float32)
     smax = np.zeros(1, np.float32)
-    assert fn(p.ctypes.data, len(p), 264, boxes.ctypes.data, smax.ctypes.data) == 0
+    assert fn(p.ctypes.data, len(p), 264, tier, boxes.ctypes.data, smax.ctypes.data) == 0
     return boxes, float(smax[0])
 
 
@@ -53,10 +57,11 @@ def random_rays(rng, n, centre, spread, far=False):
     return np.concatenate([o.T, d.T]).astype(np.float32)
 
 
-def check(bzr, orc, patches, rays):
-    boxes, smax = gate_boxes(bzr, patches)
+def check(bzr, orc, patches, rays, tier=0):
+    boxes, smax = gate_boxes(bzr, patches, tier)
     gate = orc.planar_gate(patches, rays)
     near = np.abs(rays[:3]).max(axis=0) <= smax
+    assert near.mean() > 0.5, "most test rays must start within this tier's radius"
     hit = slab_f32(boxes, rays)
     missed = gate & ~hit & near[:, None]
     assert gate.sum() > 0
@@ -64,16 +69,18 @@ def check(bzr, orc, patches, rays):
     return gate.sum(), hit.sum()
 
 
+@pytest.mark.parametrize("tier", TIERS)
 @pytest.mark.parametrize("name", ["cfg1", "cfg2", "cfg3"])
-def test_config_rays_never_culled(bzr, orc, name):
+def test_config_rays_never_culled(bzr, orc, name, tier):
     cfg = CONFIGS[name]
     patches = build_lens(bzr.TriMesh, cfg.lenses[0]).bezier_patches()
     rays = grid_rays(cfg, side=48)
-    check(bzr, orc, patches, rays)
+    check(bzr, orc, patches, rays, tier)
 
 
+@pytest.mark.parametrize("tier", TIERS)
 @pytest.mark.parametrize("seed", [1, 2, 3])
-def test_random_and_grazing_rays_never_culled(bzr, orc, seed):
+def test_random_and_grazing_rays_never_culled(bzr, orc, seed, tier):
     rng = np.random.default_rng(seed)
     patches = build_lens(bzr.TriMesh, CONFIGS["cfg2"].lenses[0]).bezier_patches()
     rays = np.concatenate([random_rays(rng, 1500, (10, 0, 0), 3.0), random_rays(rng, 500, (10, 0, 0), 3.0, far=True)], 1)
@@ -84,11 +91,12 @@ def test_random_and_grazing_rays_never_culled(bzr, orc, seed):
     d = np.array([10, 0, 0], np.float32) - o + rng.normal(0, 0.5, (500, 3)).astype(np.float32)
     d /= np.linalg.norm(d, axis=1, keepdims=True)
     rays = np.concatenate([rays, np.concatenate([o.T, d.T]).astype(np.float32)], 1)
-    gate, hit = check(bzr, orc, patches, rays)
+    gate, hit = check(bzr, orc, patches, rays, tier)
     assert hit < 0.2 * rays.shape[1] * len(patches)  # and the boxes do cull
 
 
-def test_ill_conditioned_patches(bzr, orc):
+@pytest.mark.parametrize("tier", TIERS)
+def test_ill_conditioned_patches(bzr, orc, tier):
     """Lens placed so that many patch planes pass close to the origin: the gate region is far larger than
     the flat triangle there, and the boxes must cover it."""
     m = bzr.TriMesh().make_ellipsoid(16, 8, (1.0, 4.0, 2.0)).translate((1.3, 0.5, 0.0)).standardize()
@@ -105,7 +113,7 @@ def test_ill_conditioned_patches(bzr, orc):
     d = tgt - o
     d /= np.linalg.norm(d, axis=1, keepdims=True)
     rays = np.concatenate([rays, np.concatenate([o.T, d.T]).astype(np.float32)], 1)
-    check(bzr, orc, patches, rays)
+    check(bzr, orc, patches, rays, tier)
 
 
 @pytest.mark.parametrize("cfg_name", ["cfg1", "cfg2", "cfg3"])
@@ -129,3 +137,15 @@ def test_bounding_sphere_encloses_gate_boxes(bzr, cfg_name):
     assert dist.max() <= float(sph[3])
     # and it is a useful cull: not much larger than the boxes' own extent
     assert float(sph[3]) < 1.5 * 0.5 * np.linalg.norm(hi[keep].max(0) - lo[keep].min(0)) + 1e-3
+
+
+def test_near_tier_is_tighter(bzr):
+    """The near tier exists to shrink the boxes: on cfg2 its boxes are never larger than the far
+    tier's, and smaller in total."""
+    patches = build_lens(bzr.TriMesh, CONFIGS["cfg2"].lenses[0]).bezier_patches()
+    far, s_far = gate_boxes(bzr, patches, 0)
+    near, s_near = gate_boxes(bzr, patches, 1)
+    assert s_near < s_far
+    ok = np.isfinite(far).all(axis=1) & (far[:, :3] <= far[:, 3:]).all(axis=1)
+    assert (near[ok, :3] >= far[ok, :3]).all() and (near[ok, 3:] <= far[ok, 3:]).all()
+    assert (near[ok, 3:] - near[ok, :3]).sum() < 0.99 * (far[ok, 3:] - far[ok, :3]).sum()
