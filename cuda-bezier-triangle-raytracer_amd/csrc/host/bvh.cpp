@@ -331,6 +331,12 @@ uint32_t collapse(std::vector<BvhNode> const &bin, uint32_t n2, std::vector<Bvh4
 
 }  // namespace
 
+// Patches whose gate-region box exceeds kWideRatio x their triangle's extent go to the wide subtree
+// (meshes of at least kWideMinPatches patches).
+// (64: the fewest node visits per wave on cfg5 in the host replay bzr_debug_traverse, ratios 4..512 tried.)
+constexpr float kWideRatio = 64.0f;
+constexpr uint32_t kWideMinPatches = 64;
+
 Bvh build_bvh(const float *records, uint32_t n, uint32_t stride_words, int tier) {
   Bvh out;
   std::vector<Box> box(n);
@@ -356,7 +362,41 @@ Bvh build_bvh(const float *records, uint32_t n, uint32_t stride_words, int tier)
   if (!std::isfinite(out.extent)) out.extent = HUGE_VALF;
   out.order.resize(n);
   std::iota(out.order.begin(), out.order.end(), 0u);
-  if (n) bld.build(0, n);
+  // Wide patches: gate regions much larger than their own triangle (planes through or near the
+  // origin make M ill-conditioned).  Mixed into the tree their boxes would inflate
+  // every ancestor's box and send most rays into those subtrees, so they get a subtree of their own
+  // beside the narrow patches' (root = (narrow, wide)).
+  uint32_t n_narrow = n;
+  if (n >= kWideMinPatches) {
+    auto wide = [&](uint32_t i) {
+      Box const &b = box[i];
+      if (b.empty) return false;
+      const float *cp = records + (size_t)i * stride_words + 19;
+      float tri = 0.0f, ext = 0.0f;
+      for (int a = 0; a < 3; ++a) {
+        const float lo = std::min({cp[a], cp[3 + a], cp[6 + a]}), hi = std::max({cp[a], cp[3 + a], cp[6 + a]});
+        tri = std::max(tri, hi - lo);
+        ext = std::max(ext, b.hi[a] - b.lo[a]);
+      }
+      return !(ext <= kWideRatio * tri);  // also non-finite boxes
+    };
+    auto mid = std::stable_partition(out.order.begin(), out.order.end(), [&](uint32_t i) { return !wide(i); });
+    n_narrow = static_cast<uint32_t>(mid - out.order.begin());
+  }
+  if (n && n_narrow > 0 && n_narrow < n) {
+    out.nodes.push_back({});  // root, filled below
+    const uint32_t l = bld.build(0, n_narrow), r = bld.build(n_narrow, n - n_narrow);
+    BvhNode root;
+    for (int a = 0; a < 3; ++a) {
+      root.lo[a] = std::min(out.nodes[l].lo[a], out.nodes[r].lo[a]);
+      root.hi[a] = std::max(out.nodes[l].hi[a], out.nodes[r].hi[a]);
+    }
+    root.a = l;
+    root.b = r;
+    out.nodes[0] = root;
+  } else if (n) {
+    bld.build(0, n);
+  }
   if (n) {
     collapse(out.nodes, 0, out.nodes4);
   } else {
