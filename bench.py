@@ -236,7 +236,8 @@ def main():
             "k_traverse": (seg_r0 * FLOPS_PLANAR * tests_per_seg,
                            "brute-force-equivalent planar tests 33 N_b per segment (culling skips most of them)"),
             "k_newton": (seg_r0 * FLOPS_NEWTON * newton_per_seg, "Newton stage 1750 flops per candidate pair"),
-            "k_follow": (seg_r0 * FLOPS_NEWTON * follow_per_seg, "Newton stage 1750 flops per follow-side retry"),
+            "k_follow": (seg_r0 * FLOPS_NEWTON * follow_per_seg,
+                         "k_resolve: Newton stage 1750 flops per follow-side retry (+ overflow rays' full scans)"),
             "k_finish": (seg_r0 * FLOPS_REFRACT, "Snell step 30 flops per segment"),
         }
         all_flops = sum(f for f, _ in work.values())

@@ -99,7 +99,7 @@ constexpr int kBlock = 256;
 constexpr int kWaves = kBlock / 64;
 constexpr uint32_t kMaxLenses = 8;
 #ifndef BZR_MAX_CAND
-#define BZR_MAX_CAND 24
+#define BZR_MAX_CAND 40
 #endif
 constexpr uint32_t kMaxCand = BZR_MAX_CAND;  // candidate list length per ray and segment
 constexpr uint32_t kOverflow = 0xFFFFu;  // count value: resolve with the full scan
@@ -130,7 +130,7 @@ constexpr int kTravBlock = BZR_TRAV_BLOCK;
 #ifndef BZR_NEWTON_XCD
 #define BZR_NEWTON_XCD 0
 #endif
-// Blocks of k_overflow (grid-stride over (overflow ray, patch slice) items).
+// Blocks of k_resolve at most (its overflow part is grid-stride over (overflow ray, patch slice) items).
 #ifndef BZR_OVERFLOW_BLOCKS
 #define BZR_OVERFLOW_BLOCKS 2048u
 #endif
@@ -315,8 +315,8 @@ __device__ __forceinline__ bool slab(float4 lo, float4 hi, f3 s, f3 sinv, f3 inv
 //   k_newton    the Newton stage per pair; a wave holds <= a few distinct patches, processed one at a
 //               time with the patch record in scalar registers (uniform loads); hits go to a per-pair
 //               slot and a per-ray 64-bit atomicMin on (t order key, pair index)
-//   k_follow    follow-side results: the named neighbour with cNone, per lane
-//   k_overflow  the reference's in-order scan for the overflow list, sliced over patches -> key
+//   k_resolve   follow-side results: the named neighbour with cNone, per lane; then the reference's
+//               in-order scan for the overflow list, sliced over patches -> key
 //   k_finish    winner -> BezierIntersection / refraction (overflow rays: their winner re-evaluated)
 // Pair indices are patch-major, so for one ray (t, pair index) orders like (t, scanned patch
 // index): the atomicMin winner is the reference's strict-< in-order winner.
@@ -651,21 +651,6 @@ __global__ __launch_bounds__(kBlock) void k_newton_lane(const float *__restrict_
   }
 }
 
-template <bool kFast>
-__global__ __launch_bounds__(kBlock) void k_follow(MeshView m, const float *__restrict__ rays, uint32_t ld,
-                                                   uint32_t off, Work w) {
-  const uint32_t F = __builtin_amdgcn_readfirstlane(w.ctr[0]);
-  for (uint32_t q = blockIdx.x * kBlock + threadIdx.x; q < F; q += gridDim.x * kBlock) {
-    const uint32_t f = w.fol[q], p = f & 0x3FFFFFFFu, what = f >> 30;
-    const float4 a = w.pairs[p], e = w.pairs[(size_t)w.cap + p];
-    const f3 s = mk(a.x, a.y, a.z), d = mk(e.x, e.y, e.z);
-    const uint32_t nbr = __float_as_uint(m.full[(size_t)rec::kWords * __float_as_uint(e.w) + rec::kNeigh + what]);
-    Patch pa = load_patch(m.full + (size_t)rec::kWords * nbr);
-    Hit h = patch_intersect<false, kFast>(pa, s, d, true);
-    if (h.what == kIntersect) record(w.slot, w.cap, p, h, nbr, &w.key[__float_as_uint(a.w)]);
-  }
-}
-
 template <int kMode, bool kFast>
 __global__ __launch_bounds__(kBlock) void k_finish(MeshView m, const float *rays, uint32_t ld, uint32_t off, uint32_t n,
                                                    Work w, Out o) {
@@ -678,7 +663,7 @@ __global__ __launch_bounds__(kBlock) void k_finish(MeshView m, const float *rays
   Hit h = no_hit();
   uint32_t patch = 0xFFFFFFFFu;
   const unsigned long long k = w.key[i];
-  if (w.count[i] > kMaxCand) {  // overflow ray: k_overflow left (t order, scanned patch) -- evaluate it again
+  if (w.count[i] > kMaxCand) {  // overflow ray: k_resolve left (t order, scanned patch) -- evaluate it again
     if (k != ~0ull) h = evaluate_patch<kFast>(m, static_cast<uint32_t>(k), s, d, patch);
   } else if (k != ~0ull) {
     const uint32_t p = static_cast<uint32_t>(k);
@@ -713,8 +698,23 @@ __device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v)
   return v;
 }
 
+// Follow-side retries and the overflow rays' full scans in one launch (both feed the per-ray keys
+// k_finish reads; they are independent of each other): threads first take follow requests, then
+// blocks take (overflow ray, patch slice) items.  With no overflow rays the second loop is empty --
+// one launch per segment saved over separate kernels.
 template <bool kFast>
-__global__ __launch_bounds__(kBlock) void k_overflow(MeshView m, const float *rays, uint32_t ld, uint32_t off, Work w) {
+__global__ __launch_bounds__(kBlock) void k_resolve(MeshView m, const float *__restrict__ rays, uint32_t ld,
+                                                    uint32_t off, Work w) {
+  const uint32_t F = __builtin_amdgcn_readfirstlane(w.ctr[0]);
+  for (uint32_t q = blockIdx.x * kBlock + threadIdx.x; q < F; q += gridDim.x * kBlock) {
+    const uint32_t f = w.fol[q], p = f & 0x3FFFFFFFu, what = f >> 30;
+    const float4 a = w.pairs[p], e = w.pairs[(size_t)w.cap + p];
+    const f3 s = mk(a.x, a.y, a.z), d = mk(e.x, e.y, e.z);
+    const uint32_t nbr = __float_as_uint(m.full[(size_t)rec::kWords * __float_as_uint(e.w) + rec::kNeigh + what]);
+    Patch pa = load_patch(m.full + (size_t)rec::kWords * nbr);
+    Hit h = patch_intersect<false, kFast>(pa, s, d, true);
+    if (h.what == kIntersect) record(w.slot, w.cap, p, h, nbr, &w.key[__float_as_uint(a.w)]);
+  }
   const uint32_t V = __builtin_amdgcn_readfirstlane(w.ctr[1]);
   const uint32_t S = (m.n + kOvfSlice - 1) / kOvfSlice;
   for (uint32_t item = blockIdx.x; item < V * S; item += gridDim.x) {
@@ -1014,12 +1014,10 @@ bzr_status run_culled(bzr_ctx *ctx, const MeshView &mv, const float *rays, uint3
          w.ctr, w.lanes, w.ctr + 3);
   launch(ctx, BZR_KERNEL_NEWTON_LANE, k_newton_lane<kFast>, dim3(std::min<uint32_t>(std::max<uint32_t>(n / 1024u, 1u), 1024u)),
          mv.full, w.offs + hn, w.pairs, w.slot, w.cap, w.key, w.fol, w.ctr, w.lanes, w.ctr + 3);
-  launch(ctx, BZR_KERNEL_FOLLOW, k_follow<kFast>, dim3(std::min<uint32_t>(grid_for(n / 8 + 1), 1024u)), mv, rays, ld, off,
-         w);
-  {  // overflow rays' keys are untouched by the Newton stage (their lists are empty)
+  {  // follow retries + overflow rays (whose keys the Newton stage left untouched: their lists are empty)
     const uint32_t items = n * ((nb + kOvfSlice - 1) / kOvfSlice);
-    launch(ctx, BZR_KERNEL_OVERFLOW, k_overflow<kFast>, dim3(std::max<uint32_t>(std::min<uint32_t>(items, BZR_OVERFLOW_BLOCKS), 1u)),
-           mv, rays, ld, off, w);
+    const uint32_t grid = std::max(std::min<uint32_t>(grid_for(n / 8 + 1), 1024u), std::min<uint32_t>(items, BZR_OVERFLOW_BLOCKS));
+    launch(ctx, BZR_KERNEL_FOLLOW, k_resolve<kFast>, dim3(std::max<uint32_t>(grid, 1u)), mv, rays, ld, off, w);
   }
   launch(ctx, BZR_KERNEL_FINISH, k_finish<kMode, kFast>, dim3(grid_for(n)), mv, rays, ld, off, n, w, o);
   if (ctx->counting && ctx->counters)

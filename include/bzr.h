@@ -113,9 +113,9 @@ enum {
   BZR_KERNEL_TRAVERSE = 0,        /* BVH walk + planar gate -> candidate pairs, per-patch histogram */
   BZR_KERNEL_BUCKET = 1,          /* prefix sum + scatter of the pairs into patch-major order */
   BZR_KERNEL_NEWTON = 2,          /* Newton stage per pair, patch-uniform waves */
-  BZR_KERNEL_FOLLOW = 3,          /* follow-side neighbour retries */
+  BZR_KERNEL_FOLLOW = 3,          /* k_resolve: follow-side neighbour retries + the overflow rays' full scans */
   BZR_KERNEL_FINISH = 4,          /* winner -> BezierIntersection / refraction */
-  BZR_KERNEL_OVERFLOW = 5,        /* in-order full scan for rays the culling cannot take */
+  BZR_KERNEL_OVERFLOW = 5,        /* (unused since the full scans run inside k_resolve; id kept) */
   BZR_KERNEL_INTERSECT_SCAN = 6,  /* brute force (BZR_ACCEL_NONE) */
   BZR_KERNEL_REFRACT_SCAN = 7,
   BZR_KERNEL_CHAIN_SCAN = 8,
