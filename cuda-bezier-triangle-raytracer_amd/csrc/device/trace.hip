@@ -80,6 +80,11 @@ struct bzr_ctx {
   size_t scratch_bytes = 0;
   void *work = nullptr;     // candidate lists + counts
   size_t work_bytes = 0;
+  // The culled path's counters and histogram start every segment at zero.  A segment on the small-scan
+  // path leaves them zero for the next one (k_scan_small clears the histogram it reads, k_finish the
+  // counters), so the memset is skipped while the workspace and histogram size are unchanged.
+  const uint32_t *zero_ctr = nullptr;  // workspace counters known zero, with histogram [0, zero_hn]
+  uint32_t zero_hn = 0;
   bool timing = false;      // per-kernel event timing (bzr_ctx_timing)
   struct Mark {
     int kernel;
@@ -321,8 +326,8 @@ __device__ __forceinline__ bool slab(float4 lo, float4 hi, f3 s, f3 sinv, f3 inv
 // Pair indices are patch-major, so for one ray (t, pair index) orders like (t, scanned patch
 // index): the atomicMin winner is the reference's strict-< in-order winner.
 struct Work {
-  uint32_t *hist;    // [nb + 1] pair counts per patch (hist[nb] = 0), then ctr[4]
   uint32_t *ctr;     // [0] follow count, [1] overflow count, [2] rays traced, [3] k_newton_lane chunks
+  uint32_t *hist;    // [nb + 1] pair counts per patch (hist[nb] = 0); 256 bytes after ctr
   uint32_t *offs;    // [nb + 1] exclusive prefix of hist; offs[nb] = pair count
   uint32_t *cand;    // [kMaxCand][n]
   uint32_t *rank;    // [kMaxCand][n]
@@ -348,6 +353,8 @@ struct Out {
   uint32_t *status;
   uint32_t *segments;        // kModeStage, optional
   float ri;
+  uint32_t first;            // kModeStage: the chain's first stage -- every ray is alive, its input comes
+                             // from the caller's rays and its ray / status / segments are all written here
 };
 
 template <int kMode>
@@ -357,7 +364,7 @@ __device__ __forceinline__ void emit(const Out &o, uint32_t ld, uint32_t gi, f3 
   } else {
     f3 os, od;
     uint32_t st = refract_hit(h, o.ri, s, d, o.expected ? o.expected[gi] : o.expected_all, os, od);
-    if (kMode == kModeRefract || st != BZR_RR_NONE) {
+    if (kMode == kModeRefract || st != BZR_RR_NONE || (kMode == kModeStage && o.first)) {
       if (st == BZR_RR_NONE) {
         os = s;
         od = d;
@@ -365,7 +372,7 @@ __device__ __forceinline__ void emit(const Out &o, uint32_t ld, uint32_t gi, f3 
       store_ray(o.rays, ld, gi, os, od);
     }
     o.status[gi] = st;
-    if (kMode == kModeStage && o.segments) o.segments[gi] += 1u;
+    if (kMode == kModeStage && o.segments) o.segments[gi] = o.first ? 1u : o.segments[gi] + 1u;
   }
 }
 
@@ -662,9 +669,10 @@ template <int kMode, bool kFast>
 __global__ __launch_bounds__(kBlock) void k_finish(MeshView m, const float *rays, uint32_t ld, uint32_t off, uint32_t n,
                                                    Work w, Out o) {
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (blockIdx.x == 0 && threadIdx.x < 4) w.ctr[threadIdx.x] = 0u;  // last reader of the counters this segment
   if (i >= n) return;
   const uint32_t gi = off + i;
-  if (kMode == kModeStage && o.status[gi] == BZR_RR_NONE) return;
+  if (kMode == kModeStage && !o.first && o.status[gi] == BZR_RR_NONE) return;
   f3 s, d;
   load_ray(rays, ld, gi, s, d);
   Hit h = no_hit();
@@ -757,9 +765,39 @@ __global__ void k_count(Work w, uint32_t nb, unsigned long long *__restrict__ co
   counters[BZR_COUNTER_LANE_CHUNKS] += w.ctr[3];
 }
 
-__global__ void k_fill(uint32_t *__restrict__ a, uint32_t value, uint32_t n) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) a[i] = value;
+// Exclusive prefix sum of the per-patch histogram in one block (meshes of up to kScanSmall - 1 patches;
+// larger ones use hipCUB): offs[i] = sum of hist[j < i].  It clears each histogram word it has read,
+// which leaves the histogram zero for the next segment (no memset launch).
+constexpr uint32_t kScanThreads = 1024, kScanPer = 8, kScanSmall = kScanThreads * kScanPer;
+__global__ __launch_bounds__(kScanThreads) void k_scan_small(uint32_t *__restrict__ hist, uint32_t *__restrict__ offs,
+                                                             uint32_t count) {
+  __shared__ uint32_t wave_total[kScanThreads / 64];
+  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6, base = t * kScanPer;
+  uint32_t v[kScanPer], sum = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kScanPer; ++k) {
+    v[k] = base + k < count ? hist[base + k] : 0u;
+    sum += v[k];
+  }
+  uint32_t x = sum;  // inclusive scan over the wave
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  if (lane == 63) wave_total[wv] = x;
+  __syncthreads();
+  uint32_t before = 0;
+  for (uint32_t k = 0; k < wv; ++k) before += wave_total[k];
+  uint32_t run = before + x - sum;
+#pragma unroll
+  for (uint32_t k = 0; k < kScanPer; ++k) {
+    if (base + k < count) {
+      offs[base + k] = run;
+      hist[base + k] = 0u;
+    }
+    run += v[k];
+  }
 }
 
 // ------------------------------------------------------------ brute-force path
@@ -972,14 +1010,16 @@ bzr_status ensure_work(bzr_ctx *ctx, uint32_t chunk, uint32_t nb, Work &w) {
   BZR_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, cub_bytes, static_cast<uint32_t *>(nullptr),
                                            static_cast<uint32_t *>(nullptr), hn + 1, ctx->stream));
   const size_t cap = (size_t)kMaxCand * chunk;
-  const size_t bytes = round256((size_t)(hn + 5) * 4) + round256((size_t)(hn + 1) * 4) + 2 * round256(cap * 4) +
+  const size_t bytes = round256(32) + round256((size_t)(hn + 1) * 4) + round256((size_t)(hn + 1) * 4) + 2 * round256(cap * 4) +
                        round256((size_t)chunk * 4) + round256((size_t)chunk * 8) + round256(kSlotWords * cap * 4) +
                        round256(cap * 32) + round256(cap * 4) + round256((size_t)chunk * 4) + round256((cap / 64 + 1) * 4) +
                        round256(cub_bytes);
+  const size_t had = ctx->work_bytes;
   if (bzr_status s = ensure_buffer(ctx->work, ctx->work_bytes, bytes)) return s;
+  if (ctx->work_bytes != had) ctx->zero_ctr = nullptr;  // reallocated (possibly at the same address)
   Staging st{static_cast<char *>(ctx->work)};
-  w.hist = st.take<uint32_t>(hn + 5);
-  w.ctr = w.hist + hn + 1;
+  w.ctr = st.take<uint32_t>(8);
+  w.hist = st.take<uint32_t>(hn + 1);
   w.offs = st.take<uint32_t>(hn + 1);
   w.cand = st.take<uint32_t>(cap);
   w.rank = st.take<uint32_t>(cap);
@@ -1006,12 +1046,19 @@ bzr_status run_culled(bzr_ctx *ctx, const MeshView &mv, const float *rays, uint3
                       const uint32_t *alive, const Out &o, Work &w) {
   const uint32_t nb = mv.n;
   const uint32_t hn = nb;
-  BZR_HIP(hipMemsetAsync(w.hist, 0, (size_t)(hn + 5) * 4, ctx->stream));
+  const bool small_scan = hn + 1 <= kScanSmall;
+  if (!(ctx->zero_ctr == w.ctr && ctx->zero_hn >= hn))  // counters + histogram [0, hn] to zero
+    BZR_HIP(hipMemsetAsync(w.ctr, 0, reinterpret_cast<char *>(w.hist + hn + 1) - reinterpret_cast<char *>(w.ctr),
+                           ctx->stream));
+  ctx->zero_ctr = nullptr;  // valid again only once this segment is fully enqueued
   launch_on(ctx, ctx->stream, dim3(kTravBlock), BZR_KERNEL_TRAVERSE, k_traverse, dim3((n + kTravBlock - 1) / kTravBlock),
             mv, rays, ld, off, alive, n, w, uint32_t(ctx->counting ? 1u : 0u));
   {
     Span sp(ctx, BZR_KERNEL_BUCKET);
-    BZR_HIP(hipcub::DeviceScan::ExclusiveSum(w.cub, w.cub_bytes, w.hist, w.offs, hn + 1, ctx->stream));
+    if (small_scan)
+      hipLaunchKernelGGL(k_scan_small, dim3(1), dim3(kScanThreads), 0, ctx->stream, w.hist, w.offs, hn + 1);
+    else
+      BZR_HIP(hipcub::DeviceScan::ExclusiveSum(w.cub, w.cub_bytes, w.hist, w.offs, hn + 1, ctx->stream));
     launch(ctx, -1, k_scatter, dim3(grid_for(n)), rays, ld, off, n, w);
   }
   // persistent grid: the resident capacity of the device, never more than the worst-case chunk count
@@ -1026,10 +1073,14 @@ bzr_status run_culled(bzr_ctx *ctx, const MeshView &mv, const float *rays, uint3
     const uint32_t grid = std::max(std::min<uint32_t>(grid_for(n / 8 + 1), 1024u), std::min<uint32_t>(items, BZR_OVERFLOW_BLOCKS));
     launch(ctx, BZR_KERNEL_FOLLOW, k_resolve<kFast>, dim3(std::max<uint32_t>(grid, 1u)), mv, rays, ld, off, w);
   }
-  launch(ctx, BZR_KERNEL_FINISH, k_finish<kMode, kFast>, dim3(grid_for(n)), mv, rays, ld, off, n, w, o);
-  if (ctx->counting && ctx->counters)
+  if (ctx->counting && ctx->counters)  // before k_finish, which clears the counters
     hipLaunchKernelGGL(k_count, dim3(1), dim3(64), 0, ctx->stream, w, nb, ctx->counters);
+  launch(ctx, BZR_KERNEL_FINISH, k_finish<kMode, kFast>, dim3(grid_for(n)), mv, rays, ld, off, n, w, o);
   BZR_HIP(hipGetLastError());
+  if (small_scan) {
+    ctx->zero_ctr = w.ctr;
+    ctx->zero_hn = hn;
+  }
   return BZR_OK;
 }
 
@@ -1431,9 +1482,8 @@ extern "C" bzr_status bzr_trace_chain(bzr_ctx *ctx, const bzr_mesh *const *lense
     Work w;
     const uint32_t ch = chunk_for(n);
     if (bzr_status s = ensure_work(ctx, ch, nb, w)) return s;
-    BZR_HIP(hipMemcpyAsync(d_out, d_rays, (size_t)n * 24, hipMemcpyDeviceToDevice, ctx->stream));
-    hipLaunchKernelGGL(k_fill, dim3(grid_for(n)), dim3(kBlock), 0, ctx->stream, d_st, uint32_t(BZR_RR_INSIDE), n);
-    if (d_seg) hipLaunchKernelGGL(k_fill, dim3(grid_for(n)), dim3(kBlock), 0, ctx->stream, d_seg, 0u, n);
+    // the first stage reads the caller's rays and writes every ray's ray / status / segments (no
+    // copy or fill launches); later stages update the rays in flight in place, alive = status != NONE
     for (uint32_t off = 0; off < n; off += ch) {
       const uint32_t m = std::min(ch, n - off);
       for (uint32_t l = 0; l < nlens; ++l) {
@@ -1444,7 +1494,10 @@ extern "C" bzr_status bzr_trace_chain(bzr_ctx *ctx, const bzr_mesh *const *lense
           o.status = d_st;
           o.segments = d_seg;
           o.ri = set.lens[l].ri;
-          if (bzr_status s = run_segment<kModeStage>(use_fast(flags), ctx, set.lens[l], d_out, n, off, m, d_st, o, w)) return s;
+          o.first = (l == 0 && j == 0) ? 1u : 0u;
+          if (bzr_status s = run_segment<kModeStage>(use_fast(flags), ctx, set.lens[l], o.first ? d_rays : d_out, n, off,
+                                                     m, o.first ? nullptr : d_st, o, w))
+            return s;
         }
       }
     }

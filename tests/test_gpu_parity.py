@@ -295,3 +295,27 @@ def test_cfg5_sample_against_oracle(bzr, orc, ctx):
     got = bzr.intersect(ctx, bzr.DeviceMesh(ctx, patches), rays)
     want = orc.intersect(patches, rays, threads=16)
     assert_hits_equal(got, want, "cfg5")
+
+
+def test_mixed_size_lenses_and_mesh_switching(bzr, orc, ctx, meshes):
+    """Lenses of different patch counts in one chain, and one context switching between meshes of
+    different sizes (small-scan and hipCUB paths): every segment must start from zeroed counters and
+    histogram whichever mesh ran before it."""
+    small = bzr.TriMesh().make_ellipsoid(8, 4, (1.0, 3.0, 1.5)).translate((13.0, 0.0, 0.0)).standardize()
+    lenses = [meshes["cfg2"][0], small.bezier_patches()]
+    assert len(lenses[0]) != len(lenses[1])
+    rays = grid_rays(CONFIGS["cfg2"], side=96)
+    dms = [bzr.DeviceMesh(ctx, p) for p in lenses]
+    for order in ([0, 1], [1, 0]):
+        got = bzr.trace_chain(ctx, [dms[k] for k in order], [1.3, 1.5], rays)
+        want = orc.trace_chain([lenses[k] for k in order], [1.3, 1.5], rays)
+        for g, w in zip(got, want):
+            assert np.array_equal(np.asarray(g).view(np.uint32), np.asarray(w).view(np.uint32))
+    # intersect calls alternating between a small mesh, the robot (hipCUB scan) and cfg2
+    robot = bzr.DeviceMesh(ctx, meshes["cfg3"][0])
+    seq = [(dms[1], lenses[1]), (robot, meshes["cfg3"][0]), (dms[0], lenses[0]), (dms[1], lenses[1]), (dms[0], lenses[0])]
+    r3 = grid_rays(CONFIGS["cfg3"], side=32)
+    for dm, p in seq:
+        rr = r3 if dm is robot else rays[:, :2048]
+        got = bzr.intersect(ctx, dm, rr)
+        assert np.array_equal(got.view(np.uint32), orc.intersect(p, rr).view(np.uint32))
