@@ -92,6 +92,7 @@ struct bzr_ctx {
   };
   std::vector<Mark> marks;       // recorded, not yet reported
   std::vector<hipEvent_t> spare; // event pool
+  hipEvent_t handoff = nullptr;  // orders a new stream after the previous one (bzr_ctx_set_stream)
   double ms[BZR_KERNEL_COUNT] = {};
   uint32_t calls[BZR_KERNEL_COUNT] = {};
   bool counting = false;                 // work counters (bzr_ctx_counters)
@@ -1187,6 +1188,7 @@ extern "C" bzr_status bzr_ctx_destroy(bzr_ctx *ctx) {
     (void)hipEventDestroy(mk.stop);
   }
   for (auto e : ctx->spare) (void)hipEventDestroy(e);
+  if (ctx->handoff) (void)hipEventDestroy(ctx->handoff);
   if (ctx->scratch) (void)hipFree(ctx->scratch);
   if (ctx->work) (void)hipFree(ctx->work);
   if (ctx->counters) (void)hipFree(ctx->counters);
@@ -1195,16 +1197,28 @@ extern "C" bzr_status bzr_ctx_destroy(bzr_ctx *ctx) {
   return BZR_OK;
 }
 
+namespace {
+// Switch the context's stream; work already queued on the old stream (which shares the context's
+// workspace) is ordered before anything launched on the new one.
+bzr_status switch_stream(bzr_ctx *ctx, hipStream_t next) {
+  if (next == ctx->stream) return BZR_OK;
+  DeviceGuard g(ctx->device);
+  if (!ctx->handoff) BZR_HIP(hipEventCreateWithFlags(&ctx->handoff, hipEventDisableTiming));
+  BZR_HIP(hipEventRecord(ctx->handoff, ctx->stream));
+  BZR_HIP(hipStreamWaitEvent(next, ctx->handoff, 0));
+  ctx->stream = next;
+  return BZR_OK;
+}
+}  // namespace
+
 extern "C" bzr_status bzr_ctx_set_stream(bzr_ctx *ctx, void *stream) {
   if (!ctx) return set_error(BZR_ERR_INVALID_ARGUMENT, "null context");
-  ctx->stream = reinterpret_cast<hipStream_t>(stream);
-  return BZR_OK;
+  return switch_stream(ctx, reinterpret_cast<hipStream_t>(stream));
 }
 
 extern "C" bzr_status bzr_ctx_use_own_stream(bzr_ctx *ctx) {
   if (!ctx) return set_error(BZR_ERR_INVALID_ARGUMENT, "null context");
-  ctx->stream = ctx->own;
-  return BZR_OK;
+  return switch_stream(ctx, ctx->own);
 }
 
 extern "C" bzr_status bzr_ctx_get_stream(bzr_ctx *ctx, void **stream) {

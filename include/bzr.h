@@ -102,7 +102,8 @@ bzr_status  bzr_device_count(int32_t *count);
 bzr_status bzr_ctx_create(int32_t hip_device, bzr_ctx **out);
 bzr_status bzr_ctx_destroy(bzr_ctx *ctx);
 /* Launch on a caller-owned hipStream_t (NULL = the HIP null stream);
- * bzr_ctx_use_own_stream() goes back to the context's own non-blocking stream. */
+ * bzr_ctx_use_own_stream() goes back to the context's own non-blocking stream.  Work already queued
+ * on the previous stream is ordered before later launches (an event hand-off, no host wait). */
 bzr_status bzr_ctx_set_stream(bzr_ctx *ctx, void *hip_stream);
 bzr_status bzr_ctx_use_own_stream(bzr_ctx *ctx);
 bzr_status bzr_ctx_get_stream(bzr_ctx *ctx, void **hip_stream);
