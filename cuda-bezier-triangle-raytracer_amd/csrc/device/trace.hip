@@ -479,7 +479,10 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
   const uint32_t listed = cnt <= kMaxCand ? cnt : 0u;
   // Four list slots per round: their candidate loads first, then the grouping, then all four rounds'
   // returning atomics in flight together (one wait instead of four: vmcnt retires in issue order).
-  constexpr int kRankBatch = 4;
+#ifndef BZR_RANK_BATCH
+#define BZR_RANK_BATCH 4
+#endif
+  constexpr int kRankBatch = BZR_RANK_BATCH;
   for (uint32_t j0 = 0; __any(j0 < listed); j0 += kRankBatch) {
     uint32_t b[kRankBatch], leader[kRankBatch], below[kRankBatch], base[kRankBatch];
 #pragma unroll
