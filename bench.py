@@ -1,26 +1,29 @@
 #!/usr/bin/env python3
 """Throughput benchmark: Mrays/s (primary + refracted) of the Bezier-lens refraction chain.
 
-Workload (BASELINE.json configs[1]): makeEllipsoid(32,16,(1,4,2)) lens at x=10,
-refractive index 1.3, 1024x1024 primary rays along +x from the plane x=0 over y in [-4.2,4.2],
-z in [-2.1,2.1]; each ray runs refract(INSIDE) then refract(OUTSIDE) (reference/test.cpp:376-401).
-"Rays" counts every BezierMesh::intersect call (primary + refracted segments).  --config cfg4 runs
-the two-lens 4096x4096 chain instead.
+Workload (default, BASELINE.json north_star / configs[3]): two stacked
+makeEllipsoid(32,16,(1,4,2)) lenses at x=10 and x=13, refractive index 1.3 each, 4096x4096 primary rays
+along +x from the plane x=0 over y in [-4.2,4.2], z in [-2.1,2.1]; per lens refract(INSIDE) then
+refract(OUTSIDE), a miss ends the ray (reference/test.cpp:376-401).  "Rays" counts every
+BezierMesh::intersect call (primary + refracted segments).  --config cfg2 (one lens, 1024^2), cfg3 and
+cfg5 (BezierMesh::intersect configs) are available for A/B; the driver's line is cfg4.
 
 A step = one frame: the whole chain over this rank's primary rays, inputs already resident in HBM,
 results bit-identical to the reference restatement (tests/test_gpu_parity.py).  N GPUs = N processes
-(torch.distributed over RCCL): weak scaling -- the image grows to side x (side*N) pixels, 64x64
-tiles dealt round-robin, side^2 rays per rank, and each frame's results (28 B per primary) are gathered to
-rank 0 over RCCL inside the timed region (--gather step, the default), double-buffered so frame k's
-gather overlaps frame k+1's tracing.
+(torch.distributed over RCCL).  --scaling strong (default): the fixed side x side image is dealt to the
+ranks as 64x64 tiles round-robin (the north-star's 1->8 GPU scaling on a fixed 4096^2 grid); --scaling
+weak: the image grows to side x (side*N).  With --gather rays (default) each frame's results (28 B per
+primary) are gathered to rank 0 over RCCL inside the timed region, double-buffered so frame k's gather
+overlaps frame k+1's tracing.
 
-Prints ONE JSON line on rank 0; fields are described in DESIGN.md (Measurement).
+Prints ONE JSON line on rank 0; fields are described in DESIGN.md (d).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import statistics
 import sys
 import time
 from pathlib import Path
@@ -33,10 +36,11 @@ sys.path.insert(0, str(REPO))
 
 VALU_PEAK_TFLOPS = 157.3      # MI355X FP32 vector peak (MI355X_MICROARCH.md, chip parameters)
 HBM_PEAK_GBS = 8000.0         # MI355X HBM3E peak (spec)
-FLOPS_PLANAR = 33.0           # algorithmic flops per (segment, patch) planar test
-FLOPS_NEWTON = 1750.0         # algorithmic flops per Newton candidate: bracket + 4 iterations + tail
+FLOPS_PLANAR = 33.0           # algorithmic flops per (segment, patch) planar gate
+FLOPS_NEWTON = 1750.0         # algorithmic flops per Newton run: bracket + 4 iterations + tail
 FLOPS_REFRACT = 30.0          # Snell step per segment
-BYTES_PER_PRIMARY = 24 + 32   # ray in; ray + status + segment count out
+BYTES_CHAIN = 24 + 32         # per primary: ray in; ray + status + segment count out
+BYTES_INTERSECT = 24 + 52     # per ray: ray in; BezierIntersection (13 words) out
 
 
 def parse():
@@ -44,51 +48,108 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--config", default="cfg2", choices=["cfg2", "cfg4"])
-    p.add_argument("--side", type=int, default=0, help="override rays per image side (per rank)")
-    p.add_argument("--gather", default="step", choices=["step", "none"])
+    p.add_argument("--config", default="cfg4", choices=["cfg2", "cfg3", "cfg4", "cfg5"])
+    p.add_argument("--side", type=int, default=0, help="override rays per image side")
+    p.add_argument("--scaling", default="strong", choices=["strong", "weak"])
+    p.add_argument("--gather", default="rays", choices=["rays", "none"])
     p.add_argument("--accel", default="bvh", choices=["bvh", "none"], help="none = brute-force scan (A/B)")
+    p.add_argument("--pipeline", default="fused", choices=["fused", "staged", "auto"],
+                   help="culled-path pipeline (include/bzr.h BZR_PIPELINE_*; same output bits): fused = one k_trace "
+                        "kernel per frame (default), staged = the multi-kernel path, auto = the library's choice")
     p.add_argument("--mode", default="parity", choices=["parity", "fast"],
                    help="fast = BZR_MODE_FAST Newton stage (contracted FMA, approximate div/sqrt; not bit-exact)")
     p.add_argument("--cpu-baseline", default="on", choices=["on", "off"])
-    p.add_argument("--cpu-sample-stride", type=int, default=2, help="oracle sample: every k-th row and column")
+    p.add_argument("--cpu-sample-stride", type=int, default=0,
+                   help="oracle sample: every k-th row and column (0 = per-config default)")
+    p.add_argument("--cpu-runs", type=int, default=5)
     return p.parse_args()
 
 
-def cpu_baseline(cfg, side, patches, ris, stride):
-    """The oracle (CPU restatement, test infrastructure) on a strided sample of the same workload;
-    also returns its work counters (planar tests, Newton runs) used for the algorithmic flop count."""
+def cpu_model() -> str:
+    try:
+        for line in Path("/proc/cpuinfo").read_text().splitlines():
+            if line.lower().startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_threads() -> tuple[int, str]:
+    """Host threads for the CPU baseline: every CPU this process may run on, capped by OMP_NUM_THREADS
+    when the environment sets it (the GPU pool allots a fixed CPU share per GPU and says so there)."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    if env.isdigit() and 0 < int(env) < aff:
+        return int(env), f"OMP_NUM_THREADS={env} (the host's CPU share for this process; affinity {aff})"
+    return aff, f"all {aff} CPUs in this process's affinity mask"
+
+
+def cpu_baseline(cfg, side, patches, ris, stride, runs):
+    """The oracle (CPU restatement, test infrastructure) on a strided sample of the same workload, timed as
+    BASELINE.md 2 prescribes: OpenMP over the host's threads, -O2 (reference/CMakeLists.txt:8) and
+    -O3 -march=native builds, median of `runs` runs each.  Returns the line plus the oracle's work counters."""
     from bzr_amd.configs import pixel_coords, rays_for
     from oracle import pyoracle
 
     r, c = pixel_coords(cfg, side=side, order="rows")
     keep = (r % stride == 0) & (c % stride == 0)
     rays = rays_for(cfg, r[keep], c[keep], side=side)
-    threads = min(16, os.cpu_count() or 1)
-    pyoracle.counters_reset()
-    t0 = time.perf_counter()
-    _, _, seg = pyoracle.trace_chain(patches, ris, rays, threads=threads)
-    dt = time.perf_counter() - t0
-    cnt = pyoracle.counters()
-    return {
-        "value": round(float(seg.sum()) / dt / 1e6, 4),
+    threads, why = cpu_threads()
+    builds = {"-O2": pyoracle.lib()}
+    try:
+        builds["-O3 -march=native"] = pyoracle.load_variant("-O3 -march=native", "native")
+    except Exception as e:  # noqa: BLE001 -- reported, the -O2 number still stands
+        builds["-O3 -march=native"] = None
+        native_err = str(e)[:200]
+    results, cnt = {}, None
+    for flags, L in builds.items():
+        if L is None:
+            results[flags] = {"error": native_err}
+            continue
+        times, segs = [], 0
+        for k in range(runs):
+            if flags == "-O2" and k == 0:
+                pyoracle.counters_reset()
+            t0 = time.perf_counter()
+            if cfg.op == "chain":
+                _, _, seg = pyoracle.trace_chain(patches, ris, rays, threads=threads, L=L)
+                segs = int(seg.sum())
+            else:
+                pyoracle.intersect(patches[0], rays, threads=threads, L=L)
+                segs = rays.shape[1]
+            times.append(time.perf_counter() - t0)
+            if flags == "-O2" and k == 0:
+                cnt = pyoracle.counters()
+        med = statistics.median(times)
+        results[flags] = {"median_s": round(med, 4), "runs_s": [round(t, 4) for t in times],
+                          "mrays_per_s": round(segs / med / 1e6, 4)}
+    frac = rays.shape[1] / float(side * side)
+    line = {
+        "value": results["-O2"]["mrays_per_s"],
         "unit": "Mrays/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{rays.shape[1]} primaries (every {stride}th row and column of the {side}^2 grid), "
-                  f"{int(seg.sum())} segments, {dt:.2f} s wall; oracle/bzr_oracle.c -O2, OpenMP {threads} threads",
-    }, cnt
+        "nproc": os.cpu_count(),
+        "threads_reason": why,
+        "cpu_model": cpu_model(),
+        "builds": results,
+        "sample": f"{rays.shape[1]} primaries = every {stride}th row and column of the {side}^2 grid "
+                  f"(fraction {frac:.5f}); oracle/bzr_oracle.c (CPU restatement of the reference hot path), "
+                  f"OpenMP schedule(dynamic) over {threads} threads; value = -O2 median of {runs} runs",
+    }
+    return line, cnt
 
 
-def pmc_traffic(kernel, workload, same_workload):
-    """HBM bytes per launch of `kernel` ("a+b" sums the parts) from the committed PMC profile of this
-    workload (profiles/pmc_traffic.json, written by scripts/prof_summary.py from rocprofv3 FETCH_SIZE x2
-    + WRITE_SIZE passes over bench.py).  PMC counters cannot be read from inside the timed process."""
+def pmc_traffic(kernel, workload):
+    """HBM bytes per launch of `kernel` from the committed PMC profile of this workload
+    (profiles/pmc_traffic.json, written by scripts/prof_summary.py from rocprofv3 FETCH_SIZE (x2, gfx950
+    correction) and WRITE_SIZE passes over bench.py).  PMC counters cannot be read inside the timed process."""
     path = REPO / "profiles" / "pmc_traffic.json"
-    if not same_workload or not path.exists():
+    if not path.exists():
         return None, None
-    d = json.loads(path.read_text())
-    if d.get("workload") != workload:
+    d = json.loads(path.read_text()).get("workloads", {}).get(workload)
+    if not d:
         return None, None
     parts = kernel.split("+")
     if not all(p in d["kernels"] for p in parts):
@@ -118,7 +179,9 @@ def main():
         dist.init_process_group(backend, device_id=dev if backend == "nccl" else None)
 
     cfg = CONFIGS[a.config]
+    chain = cfg.op == "chain"
     side = a.side or cfg.side
+    height = side * world if a.scaling == "weak" else side
     t0 = time.perf_counter()
     patches = [build_lens(bzr_amd.TriMesh, lens).bezier_patches() for lens in cfg.lenses]
     ris = [lens.ri for lens in cfg.lenses]
@@ -135,17 +198,24 @@ def main():
     mode = bzr_amd.ACCEL_NONE if a.accel == "none" else bzr_amd.MODE_PARITY
     if a.mode == "fast":
         mode |= bzr_amd.MODE_FAST
+    if a.accel == "bvh":
+        mode |= {"fused": bzr_amd.PIPELINE_FUSED, "staged": bzr_amd.PIPELINE_STAGED, "auto": 0}[a.pipeline]
 
-    _, _, rays_np = frame.rank_rays(cfg, rank, world, side, side * world)
+    _, _, rays_np = frame.rank_rays(cfg, rank, world, side, height)
     n = rays_np.shape[1]
     rays = torch.from_numpy(rays_np).to(dev)
-    out_rays = torch.empty((6, n), dtype=torch.float32, device=dev)
-    out_status = torch.empty(n, dtype=torch.int32, device=dev)
-    out_seg = torch.empty(n, dtype=torch.int32, device=dev)
+    if chain:
+        out_rays = torch.empty((6, n), dtype=torch.float32, device=dev)
+        out_status = torch.empty(n, dtype=torch.int32, device=dev)
+        out_seg = torch.empty(n, dtype=torch.int32, device=dev)
+    else:
+        hits = torch.empty((13, n), dtype=torch.float32, device=dev)
+    gather = world > 1 and a.gather == "rays"
+    rows = frame.PACKED_ROWS if chain else 13
     # double-buffered frame gather: frame k's packed results travel to rank 0 (RCCL, its own stream)
     # while frame k+1 is traced; a buffer is refilled only after its previous gather completed
-    packed = [torch.empty((frame.PACKED_ROWS, n), dtype=torch.float32, device=dev) for _ in range(2)]
-    gather_lists = [[torch.empty_like(packed[0]) for _ in range(world)] if (world > 1 and rank == 0) else None
+    packed = [torch.empty((rows, n), dtype=torch.float32, device=dev) for _ in range(2)] if gather else None
+    gather_lists = [[torch.empty_like(packed[0]) for _ in range(world)] if (gather and rank == 0) else None
                     for _ in range(2)]
     pending = [None, None]
     frames = [0]
@@ -153,14 +223,20 @@ def main():
     def step(ev=None):
         if ev is not None:
             ev[0].record(stream)
-        bzr_amd.trace_chain(ctx, meshes, ris, rays, out_rays, out_status, out_seg, mode=mode)
+        if chain:
+            bzr_amd.trace_chain(ctx, meshes, ris, rays, out_rays, out_status, out_seg, mode=mode)
+        else:
+            bzr_amd.intersect(ctx, meshes[0], rays, hits, mode=mode)
         if ev is not None:
             ev[1].record(stream)
-        if world > 1 and a.gather == "step":
+        if gather:
             slot = frames[0] % 2
             if pending[slot] is not None:
                 pending[slot].wait()
-            frame.pack(out_rays, out_status, out_seg, packed[slot])
+            if chain:
+                frame.pack(out_rays, out_status, out_seg, packed[slot])
+            else:
+                packed[slot].copy_(hits)
             pending[slot] = frame.gather(packed[slot], world, rank, gather_list=gather_lists[slot], async_op=True)
         frames[0] += 1
 
@@ -181,7 +257,7 @@ def main():
     drain()
     work_cnt = ctx.counters_report()
     ctx.counters(False)
-    seg_local = int(out_seg.sum().item())
+    seg_local = int(out_seg.sum().item()) if chain else n
     seg_total = torch.tensor([seg_local], dtype=torch.int64, device=dev)
     if world > 1:
         dist.all_reduce(seg_total)
@@ -219,53 +295,41 @@ def main():
         value = seg_total * a.steps / elapsed / 1e6
         base, cnt = (None, None)
         if a.cpu_baseline == "on" and world == 1:
-            base, cnt = cpu_baseline(cfg, side, patches, ris, a.cpu_sample_stride)
-        # measured on the GPU (bzr_ctx_counters, rank 0's frame); the brute-force-equivalent planar
-        # test count per segment is N_b (every patch), as SURVEY.md 8d prices it
+            stride = a.cpu_sample_stride or {"cfg2": 4, "cfg3": 32, "cfg4": 8, "cfg5": 256}[cfg.name]
+            base, cnt = cpu_baseline(cfg, side, patches, ris, stride, a.cpu_runs)
         segs = max(work_cnt["segments"], 1)
-        newton_per_seg = work_cnt["pairs"] / segs
-        follow_per_seg = work_cnt["follows"] / segs
-        tests_per_seg = float(n_patch) / len(patches)
-        if cnt and cnt["segments"]:  # cross-check with the oracle's counts on its sample
-            oracle_rates = {"newton": cnt["newton"] / cnt["segments"], "follow": cnt["follow"] / cnt["segments"]}
-        else:
-            oracle_rates = None
-        # algorithmic work per step on rank 0: F_seg = 33 N_b + 1750 (N_cand + N_follow)
-        seg_r0 = seg_local
-        work = {
-            "k_traverse": (seg_r0 * FLOPS_PLANAR * tests_per_seg,
-                           "brute-force-equivalent planar tests 33 N_b per segment (culling skips most of them)"),
-            "k_newton": (seg_r0 * FLOPS_NEWTON * newton_per_seg, "Newton stage 1750 flops per candidate pair"),
-            "k_follow": (seg_r0 * FLOPS_NEWTON * follow_per_seg,
-                         "k_resolve: Newton stage 1750 flops per follow-side retry (+ overflow rays' full scans)"),
-            "k_finish": (seg_r0 * FLOPS_REFRACT, "Snell step 30 flops per segment"),
-        }
-        all_flops = sum(f for f, _ in work.values())
-        # the Newton stage runs as k_newton (patch-uniform chunks) + k_newton_lane (fragmented chunks):
-        # priced and reported together, every Newton pair once
+        # algorithmic work of one frame on rank 0, from the GPU's own counters (bzr_ctx_counters): every
+        # planar gate the culled walk evaluated (33 flops), every Newton run (1750: cThis pairs + follow-side
+        # retries) and the Snell step per segment (30).  SURVEY.md 8d's brute-force-equivalent count
+        # (33 N_b per segment instead of the gates evaluated) is reported beside it, labelled as such.
+        newton_runs = work_cnt["pairs"] + work_cnt["follows"]
+        exec_flops = FLOPS_NEWTON * newton_runs + FLOPS_PLANAR * work_cnt["gate_tests"] + FLOPS_REFRACT * segs
+        bf_flops = FLOPS_PLANAR * n_patch / len(patches) * segs + FLOPS_NEWTON * newton_runs + FLOPS_REFRACT * segs
         if "k_newton_lane" in kernels and "k_newton" in kernels:
-            (m1, c1), (m2, c2) = kernels.pop("k_newton"), kernels.pop("k_newton_lane")
+            (m1, c1), (m2, _) = kernels.pop("k_newton"), kernels.pop("k_newton_lane")
             kernels["k_newton+k_newton_lane"] = (m1 + m2, c1)
-            work["k_newton+k_newton_lane"] = (work.pop("k_newton")[0],
-                                              "Newton stage 1750 flops per candidate pair (both kernels)")
+        work = {
+            "k_trace": (exec_flops, "culled algorithmic flops: 1750 per Newton run + 33 per planar gate evaluated "
+                                    "+ 30 per segment (GPU counters)"),
+            "k_newton+k_newton_lane": (FLOPS_NEWTON * work_cnt["pairs"], "Newton stage 1750 flops per candidate pair"),
+            "k_follow": (FLOPS_NEWTON * work_cnt["follows"], "follow-side retries, 1750 flops each"),
+            "k_finish": (FLOPS_REFRACT * segs, "Snell step 30 flops per segment"),
+        }
         per_kernel = {}
         for name, (ms, calls) in kernels.items():
             per_step = ms / a.steps
-            fl, what = work.get(name, (all_flops, "brute-force segment work F_seg"))
-            if name in ("bucket", "k_overflow"):
-                fl, what = 0.0, "bookkeeping (prefix sum + scatter) / overflow rays' full scan"
+            fl, what = work.get(name, (None, "no flop model (bookkeeping / traversal without counters)"))
             per_kernel[name] = {"ms_per_step": round(per_step, 4), "launches_per_step": calls / a.steps,
-                                "avg_launch_ms": round(ms / calls, 4),
-                                "alg_tflops": round(fl / (per_step * 1e-3) / 1e12, 3), "work": what}
-        # roofline kernel: the arithmetic stage (Newton), whose algorithmic flops are well defined.  The
-        # longer-running k_traverse is priced brute-force-equivalent, which culling
-        # beats by >1x, so its fraction says nothing about the kernel's efficiency.
-        dom_time = max(per_kernel, key=lambda k: per_kernel[k]["ms_per_step"])
-        dom = "k_newton+k_newton_lane" if "k_newton+k_newton_lane" in per_kernel else dom_time
+                                "avg_launch_ms": round(ms / calls, 4), "work": what,
+                                "alg_tflops": None if fl is None else round(fl / (per_step * 1e-3) / 1e12, 3)}
+        # roofline kernel: the one that runs longest per step
+        dom = max(per_kernel, key=lambda k: per_kernel[k]["ms_per_step"])
         d = per_kernel[dom]
         achieved = d["alg_tflops"]
-        alg_bytes = n * BYTES_PER_PRIMARY
-        traffic, traffic_src = pmc_traffic(dom, cfg.name, side == cfg.side and world == 1 and a.mode == "parity")
+        alg_bytes = n * (BYTES_CHAIN if chain else BYTES_INTERSECT)
+        workload_key = f"{cfg.name}/{a.pipeline}/{a.mode}/{side}"
+        traffic, traffic_src = pmc_traffic(dom, workload_key) if world == 1 else (None, None)
+        launches = d["launches_per_step"]
         line = {
             "metric": "Mrays/sec (primary+refracted) at 1/2/4/8 MI355X; % of HBM-read roofline",
             "value": round(value, 3),
@@ -275,18 +339,19 @@ def main():
             "warmup": a.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": a.scaling,
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (deterministic ray grid; lens built by the reference's preprocessing recipe)",
+            "data": "synthetic (deterministic ray grid; lenses built by the reference's preprocessing recipe)",
             "config": {
-                "workload": f"{cfg.name}: {cfg.note}",
-                "rays_per_gpu_side": side,
+                "workload": f"{cfg.name}: {cfg.note}" + (f" (side {side})" if side != cfg.side else ""),
+                "image": f"{side}x{height}",
                 "primaries_per_gpu": n,
                 "segments_per_step": seg_total,
                 "patches": n_patch,
-                "parallelism": f"image tiles x{world}" + (", RCCL gather of every frame to rank 0 (overlapped with the next frame)"
-                                                          if world > 1 and a.gather == "step" else ""),
+                "parallelism": f"64x64 image tiles round-robin over {world} rank(s), {a.scaling} scaling"
+                               + (", RCCL gather of every frame to rank 0 (overlapped with the next frame)" if gather else ""),
+                "pipeline": a.pipeline,
                 "scan": "BVH-culled (bit-identical to brute force)" if a.accel == "bvh" else "brute force",
                 "numerics": "parity: bit-identical to the CPU oracle" if a.mode == "parity" else
                             "fast: exact planar gate, Newton stage with FMA + approximate div/sqrt (SURVEY 8c fast gates)",
@@ -296,26 +361,37 @@ def main():
             "roofline": {
                 "bound": "valu",
                 "kernel": dom,
-                "longest_kernel": dom_time,
                 "achieved": achieved,
                 "peak": VALU_PEAK_TFLOPS,
                 "unit": "TFLOP/s",
-                "frac": round(achieved / VALU_PEAK_TFLOPS, 4),
+                "frac": None if achieved is None else round(achieved / VALU_PEAK_TFLOPS, 4),
                 "traffic": traffic,
-                "traffic_unit": "HBM bytes per launch",
+                "traffic_unit": "HBM bytes per launch (PMC)",
                 "traffic_source": traffic_src,
+                "traffic_workload": workload_key,
                 "avg_launch_ms": d["avg_launch_ms"],
                 "work": d["work"],
+                "alg_bytes_per_launch": round(alg_bytes / launches),
                 "per_kernel": per_kernel,
                 "chain_ms_hip_events": round(chain_ms, 4),
                 "hbm_alg_bytes_per_step": alg_bytes,
                 "hbm_achieved_GBps": round(alg_bytes / (chain_ms * 1e-3) / 1e9, 3),
                 "hbm_frac": round(alg_bytes / (chain_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 6),
-                "work_per_segment": {"planar_tests": round(tests_per_seg, 2), "newton": round(newton_per_seg, 4),
-                                     "follow": round(follow_per_seg, 4),
-                                     "overflow_rays_per_frame": work_cnt["overflow_rays"],
-                                     "source": "GPU counters (bzr_ctx_counters)",
-                                     "oracle_sample_rates": oracle_rates},
+                "brute_force_equiv_tflops": round(bf_flops / (chain_ms * 1e-3) / 1e12, 3),
+                "work_per_segment": {
+                    "newton_pairs": round(work_cnt["pairs"] / segs, 4),
+                    "follows": round(work_cnt["follows"] / segs, 4),
+                    "gate_tests": round(work_cnt["gate_tests"] / segs, 4),
+                    "node_visits_per_wave_segment": round(work_cnt["node_visits"] * 64 / segs, 3),
+                    "leaf_fetches_per_wave_segment": round(work_cnt["leaf_fetches"] * 64 / segs, 3),
+                    "newton_lane_utilisation": round(newton_runs / max(1, 64 * work_cnt["newton_rounds"]), 4)
+                    if work_cnt["newton_rounds"] else None,
+                    "overflow_rays_per_frame": work_cnt["overflow_rays"],
+                    "source": "GPU counters (bzr_ctx_counters), rank 0, one frame",
+                    "oracle_sample_rates": ({"newton": round(cnt["newton"] / cnt["segments"], 4),
+                                             "follow": round(cnt["follow"] / cnt["segments"], 4)}
+                                            if cnt and cnt["segments"] else None),
+                },
             },
             "cpu_baseline": base,
         }

@@ -11,12 +11,17 @@ Arrays: rays are float32 SoA [6, n] (ox, oy, oz, dx, dy, dz); hits are
 float32 [13, n] with rows t, px, py, pz, cos, b0, b1, b2, nx, ny, nz and the
 uint32 bit patterns of `what` and `patch` in rows 11 and 12.  Host numpy
 arrays or CUDA (HIP) torch tensors are accepted; tensors stay on the device
-and run asynchronously on the context's stream.
+and the call returns before the kernels finish.  Stream: a context bound with
+Context.set_stream / use_torch_stream launches there; an unbound context
+launches tensor calls on torch's current stream (so the inputs torch produced
+are ready and torch's caching allocator sees the outputs used in stream
+order), then hands its own stream an event to wait on.
 """
 from __future__ import annotations
 
 import ctypes
 import os
+from contextlib import contextmanager
 from pathlib import Path
 
 import numpy as np
@@ -29,14 +34,17 @@ OK = 0
 HOST_PTRS, DEVICE_PTRS = 0, 1
 MODE_PARITY, MODE_FAST = 0, 2
 ACCEL_NONE = 4  # brute-force scan (A/B against the default BVH-culled path)
+PIPELINE_STAGED = 8  # the culled path as separate kernels (traverse, bucket, Newton, resolve, finish)
+PIPELINE_FUSED = 16  # the culled path as one k_trace kernel (default for dense batches; see include/bzr.h)
 WHAT_FOLLOW0, WHAT_FOLLOW1, WHAT_FOLLOW2, WHAT_NONE, WHAT_INTERSECT = 0, 1, 2, 3, 4
 LIMIT_THIS, LIMIT_NONE = 0, 1
 RR_NONE, RR_INSIDE, RR_OUTSIDE = 0, 1, 2
 ENVELOPE_ELLIPSOID, ENVELOPE_TESTLENS = 0, 1
 PATCH_WORDS = 66  # sizeof(bzr_patch) / 4
 KERNELS = ("k_traverse", "bucket", "k_newton", "k_follow", "k_finish", "k_overflow", "k_intersect_scan",
-           "k_refract_scan", "k_chain_scan", "k_patch", "k_newton_lane")  # BZR_KERNEL_* ids
-COUNTERS = ("segments", "pairs", "follows", "overflow_rays", "lane_chunks")  # BZR_COUNTER_* ids
+           "k_refract_scan", "k_chain_scan", "k_patch", "k_newton_lane", "k_trace")  # BZR_KERNEL_* ids
+COUNTERS = ("segments", "pairs", "follows", "overflow_rays", "lane_chunks", "node_visits", "leaf_fetches",
+            "gate_tests", "newton_rounds")  # BZR_COUNTER_* ids
 HIT_FIELDS = 13
 
 _P = ctypes.c_void_p
@@ -176,6 +184,23 @@ def _residency(*bufs) -> int:
     return DEVICE_PTRS if flags.pop() else HOST_PTRS
 
 
+@contextmanager
+def _stream_for(ctx: "Context", residency: int):
+    """Device-buffer calls on an unbound context run on torch's current stream: the torch-made inputs are
+    ready there and the outputs are used in that stream's order (torch's caching allocator relies on
+    it).  The context's own stream is then ordered after them (event hand-off, no host wait)."""
+    if residency == DEVICE_PTRS and not ctx.bound:
+        import torch
+
+        _check(lib().bzr_ctx_set_stream(ctx.handle, torch.cuda.current_stream(ctx.device).cuda_stream or None))
+        try:
+            yield
+        finally:
+            _check(lib().bzr_ctx_use_own_stream(ctx.handle))
+    else:
+        yield
+
+
 # --------------------------------------------------------------- context
 class Context:
     """A HIP device + stream (bzr_ctx)."""
@@ -185,13 +210,17 @@ class Context:
         _check(lib().bzr_ctx_create(device, ctypes.byref(h)))
         self.handle = h
         self.device = device
+        self.bound = False  # launching on a caller stream (set_stream / use_torch_stream)
 
     def set_stream(self, stream_ptr: int | None):
-        """Launch on this hipStream_t (0 / None = the HIP null stream); None-safe."""
+        """Launch on this hipStream_t (0 / None = the HIP null stream); None-safe.  The stream must stay
+        alive while bound (include/bzr.h bzr_ctx_set_stream)."""
         _check(lib().bzr_ctx_set_stream(self.handle, stream_ptr or None))
+        self.bound = True
 
     def use_own_stream(self):
         _check(lib().bzr_ctx_use_own_stream(self.handle))
+        self.bound = False
 
     def use_torch_stream(self, stream=None):
         """Launch on a torch stream (default: torch's current stream, which may be the null stream),
@@ -281,7 +310,9 @@ def intersect(ctx: Context, mesh: DeviceMesh, rays, out=None, mode=MODE_PARITY):
     n = _n_of(rays)
     out = _empty_like(rays, HIT_FIELDS, np.float32) if out is None else out
     r, o = _Buf(rays, np.float32), _Buf(out, np.float32, True)
-    _check(lib().bzr_intersect(ctx.handle, mesh.handle, r.ptr, n, o.ptr, _residency(r, o) | mode))
+    res = _residency(r, o)
+    with _stream_for(ctx, res):
+        _check(lib().bzr_intersect(ctx.handle, mesh.handle, r.ptr, n, o.ptr, res | mode))
     return out
 
 
@@ -291,7 +322,9 @@ def patch_intersect(ctx: Context, mesh: DeviceMesh, patch_index, limit, rays, ou
     out = _empty_like(rays, HIT_FIELDS, np.float32) if out is None else out
     i, l_ = _Buf(patch_index, np.uint32), _Buf(limit, np.uint32)
     r, o = _Buf(rays, np.float32), _Buf(out, np.float32, True)
-    _check(lib().bzr_patch_intersect(ctx.handle, mesh.handle, i.ptr, l_.ptr, r.ptr, n, o.ptr, _residency(i, l_, r, o)))
+    res = _residency(i, l_, r, o)
+    with _stream_for(ctx, res):
+        _check(lib().bzr_patch_intersect(ctx.handle, mesh.handle, i.ptr, l_.ptr, r.ptr, n, o.ptr, res))
     return out
 
 
@@ -303,8 +336,10 @@ def refract(ctx: Context, mesh: DeviceMesh, ri: float, rays, expected=None, expe
     out_status = _empty_like(rays, 0, np.uint32) if out_status is None else out_status
     r, e = _Buf(rays, np.float32), _Buf(expected, np.uint32)
     o, s = _Buf(out_rays, np.float32, True), _Buf(out_status, np.uint32, True)
-    _check(lib().bzr_refract(ctx.handle, mesh.handle, float(ri), r.ptr, e.ptr, int(expected_all), n, o.ptr, s.ptr,
-                             _residency(r, o, s, *([e] if expected is not None else [])) | mode))
+    res = _residency(r, o, s, *([e] if expected is not None else []))
+    with _stream_for(ctx, res):
+        _check(lib().bzr_refract(ctx.handle, mesh.handle, float(ri), r.ptr, e.ptr, int(expected_all), n, o.ptr, s.ptr,
+                                 res | mode))
     return out_rays, out_status
 
 
@@ -319,8 +354,10 @@ def trace_chain(ctx: Context, lenses, ri, rays, out_rays=None, out_status=None, 
     out_segments = _empty_like(rays, 0, np.uint32) if out_segments is None else out_segments
     r = _Buf(rays, np.float32)
     o, s, g = _Buf(out_rays, np.float32, True), _Buf(out_status, np.uint32, True), _Buf(out_segments, np.uint32, True)
-    _check(lib().bzr_trace_chain(ctx.handle, ctypes.cast(handles, _P), ctypes.cast(ris, _P), nl, r.ptr, n, o.ptr, s.ptr,
-                                 g.ptr, _residency(r, o, s, g) | mode))
+    res = _residency(r, o, s, g)
+    with _stream_for(ctx, res):
+        _check(lib().bzr_trace_chain(ctx.handle, ctypes.cast(handles, _P), ctypes.cast(ris, _P), nl, r.ptr, n, o.ptr,
+                                     s.ptr, g.ptr, res | mode))
     return out_rays, out_status, out_segments
 
 
@@ -350,7 +387,9 @@ def interpolate(ctx: Context, mesh: DeviceMesh, divisor: int, out=None):
     if out is None:
         out = np.empty((count, 3, 3), np.float32)
     o = _Buf(out, np.float32, True)
-    _check(lib().bzr_mesh_interpolate(ctx.handle, mesh.handle, int(divisor), o.ptr, _residency(o)))
+    res = _residency(o)
+    with _stream_for(ctx, res):
+        _check(lib().bzr_mesh_interpolate(ctx.handle, mesh.handle, int(divisor), o.ptr, res))
     return out
 
 
@@ -376,7 +415,9 @@ def emit(ctx: Context, em: Emitter, first: int, n: int, rays=None, patch=None):
     rays = np.empty((6, n), np.float32) if rays is None else rays
     patch = np.empty(n, np.uint32) if patch is None else patch
     r, p = _Buf(rays, np.float32, True), _Buf(patch, np.uint32, True)
-    _check(lib().bzr_emit(ctx.handle, ctypes.byref(em), int(first), int(n), r.ptr, p.ptr, _residency(r, p)))
+    res = _residency(r, p)
+    with _stream_for(ctx, res):
+        _check(lib().bzr_emit(ctx.handle, ctypes.byref(em), int(first), int(n), r.ptr, p.ptr, res))
     return rays, patch
 
 
@@ -389,8 +430,10 @@ def illuminate(ctx: Context, lenses, ri, em: Emitter, total_rays: int, target: T
     hist = np.zeros((target.bins_v, target.bins_u), np.uint32) if hist is None else hist
     h = _Buf(hist, np.uint32, True)
     stats = (ctypes.c_uint64 * 4)()
-    _check(lib().bzr_illuminate(ctx.handle, handles, ris, nl, ctypes.byref(em), int(total_rays), ctypes.byref(target),
-                                h.ptr, stats, _residency(h)))
+    res = _residency(h)
+    with _stream_for(ctx, res):
+        _check(lib().bzr_illuminate(ctx.handle, handles, ris, nl, ctypes.byref(em), int(total_rays),
+                                    ctypes.byref(target), h.ptr, stats, res))
     return hist, dict(zip(ILLUM_STATS, [int(x) for x in stats]))
 
 

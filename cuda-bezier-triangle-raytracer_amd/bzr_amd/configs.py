@@ -12,8 +12,8 @@ from pathlib import Path
 
 import numpy as np
 
-REPO = Path(__file__).resolve().parents[2]
-ROBOT_STL = REPO / "tests" / "golden" / "robot.stl"  # copy of reference/robot.stl (150 binary STL triangles)
+# package data: copy of reference/robot.stl (150 binary STL triangles), the input mesh of cfg3
+ROBOT_STL = Path(__file__).resolve().parent / "data" / "robot.stl"
 
 
 @dataclass(frozen=True)

@@ -736,8 +736,9 @@ __global__ __launch_bounds__(kBlock) void k_resolve(MeshView m, const float *__r
   }
   const uint32_t V = __builtin_amdgcn_readfirstlane(w.ctr[1]);
   const uint32_t S = (m.n + kOvfSlice - 1) / kOvfSlice;
-  for (uint32_t item = blockIdx.x; item < V * S; item += gridDim.x) {
-    const uint32_t q = item / S, lo = (item - q * S) * kOvfSlice, hi = min(m.n, lo + kOvfSlice);
+  const uint64_t items = (uint64_t)V * S;  // 64-bit: 2^20-ray chunks x slices of meshes above ~8M patches
+  for (uint64_t item = blockIdx.x; item < items; item += gridDim.x) {
+    const uint32_t q = (uint32_t)(item / S), lo = (uint32_t)(item - (uint64_t)q * S) * kOvfSlice, hi = min(m.n, lo + kOvfSlice);
     const uint32_t i = w.ovf[q];
     f3 s, d;
     load_ray(rays, ld, off + i, s, d);
@@ -801,6 +802,265 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_small(uint32_t *__restric
       hist[base + k] = 0u;
     }
     run += v[k];
+  }
+}
+
+// ------------------------------------------------------------ fused path (default)
+// One kernel per call: each wave takes 64 rays and runs every segment of them (one BezierMesh::intersect,
+// or the whole refraction chain) without leaving the wave.  The wave walks the lens BVH as k_traverse
+// does; each leaf whose exact planar gate passes for some lanes is queued (wave-uniform patch index +
+// lane mask, at most the 4 children of one node), and the queue is drained through ONE Newton site:
+// the lanes that passed run BezierTriangle::intersect with the patch record in SGPRs (uniform
+// constant-address loads), then, side by side, the follow-side retries on the named neighbours
+// (reference/bezierMesh.cpp:212-216; the neighbour of side K is uniform too).  Each lane keeps the
+// lexicographic minimum of (t order key, scanned patch index) -- the reference's strict-< in-order
+// winner, as in the staged path -- with the winning hit in LDS.  Nothing per pair leaves the CU: HBM
+// sees the rays in and the results out.  A patch sits in one leaf, so a wave runs Newton at most once
+// per (patch, segment); the lanes that do not need it idle through that pass (lane utilisation is the
+// wave's pairs / (64 x distinct patches)).  Rays whose origin lies beyond the tree's
+// validity radius, or whose stack overflows, take the reference's in-order scan in the same wave
+// (same Newton site, patches in index order).
+// Device work counters (bzr_ctx_counters) are kept in this many copies, summed by the report: a wave adds
+// to copy (wave index mod kCounterReplicas), so a frame's ~10^5 waves do not queue on 8 addresses.
+constexpr uint32_t kCounterReplicas = 64;
+struct TraceCtr {  // wave-uniform work counters (kCount)
+  uint32_t nodes = 0, leaves = 0, gate_tests = 0, rounds = 0, pairs = 0, follows = 0, segments = 0, ovf = 0;
+};
+constexpr int kHitWords = 12;  // t, point, cos, bary, normal, source patch
+struct TraceLds {              // per wave
+  uint32_t stack[kStack];
+  float hit[kHitWords][64];    // the lane's current winner (written only when it improves)
+};
+
+__device__ __forceinline__ uint32_t popc64(unsigned long long m) { return (uint32_t)__popcll(m); }
+
+// The lane's candidate `h` from scanned patch `scan` (the hit itself from patch `src`).
+__device__ __forceinline__ void consider(const Hit &h, uint32_t scan, uint32_t src, unsigned long long &best,
+                                         TraceLds &L, uint32_t lane) {
+  if (h.what == kIntersect && h.t < FLT_MAX) {
+    const unsigned long long k = ((unsigned long long)t_order(h.t) << 32) | scan;
+    if (k < best) {
+      best = k;
+      L.hit[0][lane] = h.t;
+      L.hit[1][lane] = h.point.x;
+      L.hit[2][lane] = h.point.y;
+      L.hit[3][lane] = h.point.z;
+      L.hit[4][lane] = h.cs;
+      L.hit[5][lane] = h.bary.x;
+      L.hit[6][lane] = h.bary.y;
+      L.hit[7][lane] = h.bary.z;
+      L.hit[8][lane] = h.normal.x;
+      L.hit[9][lane] = h.normal.y;
+      L.hit[10][lane] = h.normal.z;
+      L.hit[11][lane] = __uint_as_float(src);
+    }
+  }
+}
+
+// One BezierMesh::intersect for the wave's active lanes; the winner is left in `best` / L.hit.
+template <bool kFast, bool kCount>
+__device__ __forceinline__ void trace_segment(const MeshView &m, f3 s, f3 d, bool act, unsigned long long &best,
+                                              TraceLds &L, uint32_t lane, TraceCtr &ctr) {
+  best = ~0ull;
+  const float amax = fmaxf(fmaxf(fabsf(s.x), fabsf(s.y)), fabsf(s.z));
+  bool ovf = false;  // this lane takes the in-order full scan
+  if (act && !(amax <= m.s_max)) {
+    ovf = true;
+    act = false;
+  }
+  const bool near_tier = !__any(act && !(amax <= m.s_near));
+  const bzr_host::Bvh4Node *nodes = near_tier ? m.nodes_near : m.nodes;
+  const float4 *leaf = near_tier ? m.leaf_near : m.leaf;
+  const f3 inv = mk(safe_inv(d.x), safe_inv(d.y), safe_inv(d.z));
+  const f3 sinv = mk(s.x * inv.x, s.y * inv.y, s.z * inv.z);
+  int sp = 0;
+  if (m.n > 0 && __any(act)) {
+    L.stack[0] = 0u;
+    sp = 1;
+  }
+  // leaf queue: wave-uniform patch indices + per-lane gate results (LIFO, fixed slots)
+  uint32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0, qn = 0;
+  bool p0 = false, p1 = false, p2 = false, p3 = false;
+  uint32_t scan = 0xFFFFFFFFu;  // next patch of the full scan (0xFFFFFFFF: not scanning)
+  for (;;) {
+    if (qn == 0) {
+      if (sp > 0) {
+        const uint32_t node = __builtin_amdgcn_readfirstlane(L.stack[--sp]);
+        const cu32x16 *np = (const cu32x16 *)(uintptr_t)(nodes + node);
+        const u32x16 na = np[0], nb = np[1];
+        if (kCount) ++ctr.nodes;
+        bool hit[4];
+        uint32_t ch[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const float4 lo = make_float4(__uint_as_float(na[c]), __uint_as_float(na[4 + c]), __uint_as_float(na[8 + c]), 0.0f);
+          const float4 hi = make_float4(__uint_as_float(na[12 + c]), __uint_as_float(nb[c]), __uint_as_float(nb[4 + c]), 0.0f);
+          ch[c] = nb[8 + c];
+          hit[c] = act & (ch[c] != bzr_host::kEmptyChild) & slab(lo, hi, s, sinv, inv);
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const unsigned long long hm = __ballot(hit[c]);
+          if (hm == 0ull) continue;
+          if (ch[c] & bzr_host::kLeafFlag) {
+            const u32x16 r = *((const cu32x16 *)(uintptr_t)leaf + (ch[c] & ~bzr_host::kLeafFlag));
+            const float4 g0 = make_float4(__uint_as_float(r[0]), __uint_as_float(r[1]), __uint_as_float(r[2]), __uint_as_float(r[3]));
+            const float4 g1 = make_float4(__uint_as_float(r[4]), __uint_as_float(r[5]), __uint_as_float(r[6]), __uint_as_float(r[7]));
+            const float4 g2 = make_float4(__uint_as_float(r[8]), __uint_as_float(r[9]), __uint_as_float(r[10]), __uint_as_float(r[11]));
+            const float4 g3 = make_float4(__uint_as_float(r[12]), __uint_as_float(r[13]), __uint_as_float(r[14]), 0.0f);
+            const bool pass = hit[c] && planar_gate(g0, g1, g2, g3, s, d);
+            if (kCount) {
+              ++ctr.leaves;
+              ctr.gate_tests += popc64(hm);
+            }
+            if (__any(pass)) {
+              q3 = q2; q2 = q1; q1 = q0; q0 = r[15];
+              p3 = p2; p2 = p1; p1 = p0; p0 = pass;
+              ++qn;
+            }
+          } else if (sp < kStack) {
+            L.stack[sp++] = ch[c];
+          } else {  // traversal stack exhausted: these lanes take the full scan
+            if (hit[c]) ovf = true;
+          }
+        }
+        continue;
+      }
+      // tree done: the reference's in-order scan for the lanes that could not use it
+      if (scan == 0xFFFFFFFFu) {
+        if (!__any(ovf)) break;
+        scan = 0;
+        if (kCount) ctr.ovf += popc64(__ballot(ovf));
+      }
+      bool pass = false;
+      for (; scan < m.n; ++scan) {
+        const float4 *g = m.planar + 4u * scan;  // wave-uniform address -> scalar loads
+        pass = ovf && planar_gate(g[0], g[1], g[2], g[3], s, d);
+        if (__any(pass)) break;
+      }
+      if (scan >= m.n) break;
+      q0 = scan++;
+      p0 = pass;
+      qn = 1;
+    }
+    // Newton site: the queue head's patch for the lanes that passed its gate, then its follow-side
+    // neighbours (limit cNone) for the lanes that asked for them; all ordered by the head's index.
+    const uint32_t b = q0;
+    const bool run0 = p0;
+    q0 = q1; q1 = q2; q2 = q3;
+    p0 = p1; p1 = p2; p2 = p3;
+    --qn;
+    const auto hp = uniform_patch(m.full, b);
+    uint32_t pb = b, side = 0, what = kNone;
+    bool lim = false, run = run0;
+    for (;;) {
+      if (kCount) {
+        ++ctr.rounds;
+        if (lim) ctr.follows += popc64(__ballot(run));
+        else ctr.pairs += popc64(__ballot(run));
+      }
+      const auto pa = uniform_patch(m.full, pb);
+      if (run) {
+        const Hit h = patch_intersect<false, kFast>(pa, s, d, lim);
+        consider(h, b, pb, best, L, lane);
+        if (!lim) what = h.what;
+      }
+      while (side < 3u && !__any(run0 && what == side)) ++side;
+      if (side >= 3u) break;
+      pb = __float_as_uint(hp.r[rec::kNeigh + side]);
+      run = run0 && what == side;
+      lim = true;
+      ++side;
+    }
+  }
+}
+
+// Trace job of one launch.  Modes: kModeHits (one BezierMesh::intersect per ray -> hits), kModeRefract
+// (one BezierLens::refract -> ray', status), kModeStage (the chain over lenses [0, count): refract(INSIDE)
+// then refract(OUTSIDE) per lens, a NONE ends the ray -- reference/test.cpp:376-401).
+struct TraceJob {
+  const float *rays;         // input [6][n]
+  float *hits;               // kModeHits [13][n]
+  float *out_rays;           // kModeRefract / kModeStage [6][n] (may alias rays in kModeStage)
+  uint32_t *status;          // kModeRefract / kModeStage [n]
+  uint32_t *segments;        // kModeStage, optional [n]
+  const uint32_t *expected;  // kModeRefract: per ray, or null -> expected_all
+  const uint32_t *alive_in;  // kModeStage: rays with alive_in[i] == NONE are skipped and left untouched
+  uint32_t expected_all;
+  uint32_t n;
+  uint32_t ld;               // row stride of rays / out_rays / hits (>= n)
+};
+
+template <int kMode, bool kFast, bool kCount>
+__global__ __launch_bounds__(kBlock) void k_trace(LensSet lenses, TraceJob job, unsigned long long *__restrict__ counters) {
+  __shared__ TraceLds lds[kWaves];
+  const uint32_t lane = threadIdx.x & 63u;
+  TraceLds &L = lds[threadIdx.x >> 6];
+  const uint32_t i = xcd_contiguous(blockIdx.x, gridDim.x) * kBlock + threadIdx.x;
+  const uint32_t n = job.n;
+  TraceCtr ctr;
+  bool alive = i < n;
+  if (kMode == kModeStage && job.alive_in && alive) alive = job.alive_in[i] != BZR_RR_NONE;
+  const bool traced = alive;
+  f3 s = mk(0.0f, 0.0f, 0.0f), d = s;
+  if (i < n) load_ray(job.rays, job.ld, i, s, d);
+  const uint32_t nseg = kMode == kModeStage ? 2u * lenses.count : 1u;
+  uint32_t st = BZR_RR_NONE, seg = 0;
+  for (uint32_t k = 0; k < nseg; ++k) {
+    if (!__any(alive)) break;
+    const MeshView &m = lenses.lens[k >> 1];
+    unsigned long long best;
+    trace_segment<kFast, kCount>(m, s, d, alive, best, L, lane, ctr);
+    if (kCount) ctr.segments += popc64(__ballot(alive));
+    Hit h = no_hit();
+    uint32_t patch = 0xFFFFFFFFu;
+    if (best != ~0ull) {
+      h.t = L.hit[0][lane];
+      h.point = mk(L.hit[1][lane], L.hit[2][lane], L.hit[3][lane]);
+      h.cs = L.hit[4][lane];
+      h.bary = mk(L.hit[5][lane], L.hit[6][lane], L.hit[7][lane]);
+      h.normal = mk(L.hit[8][lane], L.hit[9][lane], L.hit[10][lane]);
+      h.what = kIntersect;
+      patch = __float_as_uint(L.hit[11][lane]);
+    }
+    if (kMode == kModeHits) {
+      if (alive) store_hit(job.hits, job.ld, i, h, patch);
+    } else {
+      const uint32_t expected = kMode == kModeRefract ? (job.expected ? (alive ? job.expected[i] : 0u) : job.expected_all)
+                                                      : ((k & 1u) ? uint32_t(BZR_RR_OUTSIDE) : uint32_t(BZR_RR_INSIDE));
+      f3 os, od;
+      const uint32_t r = refract_hit(h, m.ri, s, d, expected, os, od);
+      if (alive) {
+        ++seg;
+        st = r;
+        if (r == BZR_RR_NONE) alive = false;
+        else {
+          s = os;
+          d = od;
+        }
+      }
+    }
+  }
+  if (kMode != kModeHits && traced) {
+    store_ray(job.out_rays, job.ld, i, s, d);
+    job.status[i] = st;
+    if (kMode == kModeStage && job.segments) job.segments[i] = seg;
+  }
+  if (kCount && lane < 8u) {  // one atomic per counter per wave, spread over kCounterReplicas copies
+    const uint32_t v[8] = {ctr.segments, ctr.pairs, ctr.follows, ctr.ovf, ctr.nodes, ctr.leaves, ctr.gate_tests,
+                           ctr.rounds};
+    const uint32_t id[8] = {BZR_COUNTER_SEGMENTS, BZR_COUNTER_PAIRS, BZR_COUNTER_FOLLOWS, BZR_COUNTER_OVERFLOW_RAYS,
+                            BZR_COUNTER_NODE_VISITS, BZR_COUNTER_LEAF_FETCHES, BZR_COUNTER_GATE_TESTS,
+                            BZR_COUNTER_NEWTON_ROUNDS};
+    uint32_t mine = 0, which = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 8u; ++k)
+      if (lane == k) {
+        mine = v[k];
+        which = id[k];
+      }
+    const uint32_t rep = (blockIdx.x * kWaves + (threadIdx.x >> 6)) % kCounterReplicas;
+    if (mine) atomicAdd(&counters[(size_t)rep * BZR_COUNTER_COUNT + which], (unsigned long long)mine);
   }
 }
 
@@ -932,6 +1192,16 @@ bzr_status check_ctx_mesh(bzr_ctx *ctx, const bzr_mesh *mesh) {
 
 bool use_scan(uint32_t flags) { return (flags & BZR_ACCEL_NONE) != 0; }
 bool use_fast(uint32_t flags) { return (flags & BZR_MODE_FAST) != 0; }
+// Culled-path pipeline for a call of n rays over meshes of at most nb patches (include/bzr.h): forced by
+// BZR_PIPELINE_STAGED / BZR_PIPELINE_FUSED, otherwise fused for dense batches (rays per patch >= 2048:
+// cfg4 at 4096^2 has 5461 and a wave's 64 rays meet ~2 patches per segment; cfg2 at 1024^2 has 341 and
+// the staged path is 1.8x faster there).
+constexpr uint64_t kFusedRaysPerPatch = 2048;
+bool use_staged(uint32_t flags, uint64_t n, uint64_t nb) {
+  if (flags & BZR_PIPELINE_STAGED) return true;
+  if (flags & BZR_PIPELINE_FUSED) return false;
+  return n < kFusedRaysPerPatch * nb;
+}
 // BZR_MODE_FAST runs on the culled pipeline's kernels only; the brute-force scan is the parity reference.
 bzr_status check_flags(uint32_t flags) {
   if (use_fast(flags) && use_scan(flags))
@@ -1073,8 +1343,9 @@ bzr_status run_culled(bzr_ctx *ctx, const MeshView &mv, const float *rays, uint3
   launch(ctx, BZR_KERNEL_NEWTON_LANE, k_newton_lane<kFast>, dim3(std::min<uint32_t>(std::max<uint32_t>(n / 1024u, 1u), 1024u)),
          mv.full, w.offs + hn, w.pairs, w.slot, w.cap, w.key, w.fol, w.ctr, w.lanes, w.ctr + 3);
   {  // follow retries + overflow rays (whose keys the Newton stage left untouched: their lists are empty)
-    const uint32_t items = n * ((nb + kOvfSlice - 1) / kOvfSlice);
-    const uint32_t grid = std::max(std::min<uint32_t>(grid_for(n / 8 + 1), 1024u), std::min<uint32_t>(items, BZR_OVERFLOW_BLOCKS));
+    const uint64_t items = (uint64_t)n * ((nb + kOvfSlice - 1) / kOvfSlice);
+    const uint32_t grid = std::max(std::min<uint32_t>(grid_for(n / 8 + 1), 1024u),
+                                   (uint32_t)std::min<uint64_t>(items, BZR_OVERFLOW_BLOCKS));
     launch(ctx, BZR_KERNEL_FOLLOW, k_resolve<kFast>, dim3(std::max<uint32_t>(grid, 1u)), mv, rays, ld, off, w);
   }
   if (ctx->counting && ctx->counters)  // before k_finish, which clears the counters
@@ -1086,6 +1357,36 @@ bzr_status run_culled(bzr_ctx *ctx, const MeshView &mv, const float *rays, uint3
     ctx->zero_hn = hn;
   }
   return BZR_OK;
+}
+
+// The fused path: one k_trace launch for the whole job (no workspace, no chunking).
+template <int kMode>
+bzr_status run_fused(bzr_ctx *ctx, const LensSet &set, const TraceJob &job, uint32_t flags) {
+  if (job.n == 0) return BZR_OK;
+  const bool fast = use_fast(flags), count = ctx->counting && ctx->counters;
+  const dim3 grid(grid_for(job.n));
+  if (fast) {
+    if (count) launch(ctx, BZR_KERNEL_TRACE, k_trace<kMode, true, true>, grid, set, job, ctx->counters);
+    else launch(ctx, BZR_KERNEL_TRACE, k_trace<kMode, true, false>, grid, set, job, ctx->counters);
+  } else {
+    if (count) launch(ctx, BZR_KERNEL_TRACE, k_trace<kMode, false, true>, grid, set, job, ctx->counters);
+    else launch(ctx, BZR_KERNEL_TRACE, k_trace<kMode, false, false>, grid, set, job, ctx->counters);
+  }
+  BZR_HIP(hipGetLastError());
+  return BZR_OK;
+}
+
+uint32_t max_patches(const LensSet &set) {
+  uint32_t nb = 0;
+  for (uint32_t l = 0; l < set.count; ++l) nb = std::max(nb, set.lens[l].n);
+  return nb;
+}
+
+LensSet single_lens(const MeshView &mv) {
+  LensSet set{};
+  set.count = 1;
+  set.lens[0] = mv;
+  return set;
 }
 
 template <int kMode>
@@ -1161,8 +1462,9 @@ extern "C" bzr_status bzr_ctx_counters(bzr_ctx *ctx, int32_t enable) {
   if (!ctx) return set_error(BZR_ERR_INVALID_ARGUMENT, "null context");
   DeviceGuard g(ctx->device);
   if (enable && !ctx->counters) {
-    BZR_HIP(hipMalloc(&ctx->counters, BZR_COUNTER_COUNT * sizeof(unsigned long long)));
-    BZR_HIP(hipMemsetAsync(ctx->counters, 0, BZR_COUNTER_COUNT * sizeof(unsigned long long), ctx->stream));
+    BZR_HIP(hipMalloc(&ctx->counters, kCounterReplicas * BZR_COUNTER_COUNT * sizeof(unsigned long long)));
+    BZR_HIP(hipMemsetAsync(ctx->counters, 0, kCounterReplicas * BZR_COUNTER_COUNT * sizeof(unsigned long long),
+                           ctx->stream));
   }
   ctx->counting = enable != 0;
   return BZR_OK;
@@ -1173,11 +1475,13 @@ extern "C" bzr_status bzr_ctx_counters_report(bzr_ctx *ctx, uint64_t counts[BZR_
   for (int k = 0; k < BZR_COUNTER_COUNT; ++k) counts[k] = 0;
   if (!ctx->counters) return BZR_OK;
   DeviceGuard g(ctx->device);
-  unsigned long long host[BZR_COUNTER_COUNT];
-  BZR_HIP(hipMemcpyAsync(host, ctx->counters, sizeof(host), hipMemcpyDeviceToHost, ctx->stream));
-  BZR_HIP(hipMemsetAsync(ctx->counters, 0, sizeof(host), ctx->stream));
+  std::vector<unsigned long long> host((size_t)kCounterReplicas * BZR_COUNTER_COUNT);
+  const size_t bytes = host.size() * sizeof(unsigned long long);
+  BZR_HIP(hipMemcpyAsync(host.data(), ctx->counters, bytes, hipMemcpyDeviceToHost, ctx->stream));
+  BZR_HIP(hipMemsetAsync(ctx->counters, 0, bytes, ctx->stream));
   BZR_HIP(hipStreamSynchronize(ctx->stream));
-  for (int k = 0; k < BZR_COUNTER_COUNT; ++k) counts[k] = host[k];
+  for (uint32_t r = 0; r < kCounterReplicas; ++r)
+    for (int k = 0; k < BZR_COUNTER_COUNT; ++k) counts[k] += host[(size_t)r * BZR_COUNTER_COUNT + k];
   return BZR_OK;
 }
 
@@ -1349,6 +1653,12 @@ extern "C" bzr_status bzr_intersect(bzr_ctx *ctx, const bzr_mesh *mesh, const fl
   MeshView mv = view_of(mesh);
   if (use_scan(flags)) {
     launch(ctx, BZR_KERNEL_INTERSECT_SCAN, k_intersect_scan, dim3(grid_for(n)), mv, d_rays, n, d_hits);
+  } else if (!use_staged(flags, n, mesh->n)) {
+    TraceJob job{};
+    job.rays = d_rays;
+    job.hits = d_hits;
+    job.n = job.ld = n;
+    if (bzr_status s = run_fused<kModeHits>(ctx, single_lens(mv), job, flags)) return s;
   } else {
     Work w;
     const uint32_t ch = chunk_for(n);
@@ -1434,6 +1744,15 @@ extern "C" bzr_status bzr_refract(bzr_ctx *ctx, const bzr_mesh *mesh, float ri, 
   if (use_scan(flags)) {
     launch(ctx, BZR_KERNEL_REFRACT_SCAN, k_refract_scan, dim3(grid_for(n)), mv, d_rays, d_exp, expected_all,
                        n, d_out, d_st);
+  } else if (!use_staged(flags, n, mesh->n)) {
+    TraceJob job{};
+    job.rays = d_rays;
+    job.out_rays = d_out;
+    job.status = d_st;
+    job.expected = d_exp;
+    job.expected_all = expected_all;
+    job.n = job.ld = n;
+    if (bzr_status s = run_fused<kModeRefract>(ctx, single_lens(mv), job, flags)) return s;
   } else {
     Work w;
     const uint32_t ch = chunk_for(n);
@@ -1492,6 +1811,14 @@ extern "C" bzr_status bzr_trace_chain(bzr_ctx *ctx, const bzr_mesh *const *lense
   if (use_scan(flags)) {
     launch(ctx, BZR_KERNEL_CHAIN_SCAN, k_chain_scan, dim3(grid_for(n)), set, d_rays, n, d_out, d_st, d_seg);
     BZR_HIP(hipGetLastError());
+  } else if (!use_staged(flags, n, max_patches(set))) {
+    TraceJob job{};
+    job.rays = d_rays;
+    job.out_rays = d_out;
+    job.status = d_st;
+    job.segments = d_seg;
+    job.n = job.ld = n;
+    if (bzr_status s = run_fused<kModeStage>(ctx, set, job, flags)) return s;
   } else {
     // stage by stage: out_rays holds the rays in flight, out_status != NONE marks them alive
     uint32_t nb = 0;
@@ -1772,23 +2099,37 @@ extern "C" bzr_status bzr_illuminate(bzr_ctx *ctx, const bzr_mesh *const *lenses
   BZR_HIP(hipMemsetAsync(d_stats, 0, 32, ctx->stream));
   if (host) BZR_HIP(hipMemsetAsync(d_hist, 0, cells * 4, ctx->stream));
   Work w;
-  if (bzr_status s = ensure_work(ctx, B, nb, w)) return s;
+  const bool staged = use_staged(flags, B, nb);
+  if (staged)
+    if (bzr_status s = ensure_work(ctx, B, nb, w)) return s;
   const float4 sphere = make_float4(lenses[0]->sphere[0], lenses[0]->sphere[1], lenses[0]->sphere[2],
                                     lenses[0]->sphere[3]);
   for (uint64_t first = 0; first < total_rays; first += B) {
     const uint32_t m = (uint32_t)std::min<uint64_t>(B, total_rays - first);
     hipLaunchKernelGGL(k_emit, dim3(grid_for(m)), dim3(kBlock), 0, ctx->stream, *em, bt, first, m, B, d_rays,
                        (uint32_t *)nullptr, d_st, d_seg, sphere, d_stats);
-    for (uint32_t l = 0; l < nlens; ++l)
-      for (uint32_t j = 0; j < 2; ++j) {
-        Out o{};
-        o.rays = d_rays;
-        o.expected_all = j == 0 ? uint32_t(BZR_RR_INSIDE) : uint32_t(BZR_RR_OUTSIDE);
-        o.status = d_st;
-        o.segments = d_seg;
-        o.ri = set.lens[l].ri;
-        if (bzr_status s = run_segment<kModeStage>(use_fast(flags), ctx, set.lens[l], d_rays, B, 0, m, d_st, o, w)) return s;
-      }
+    if (!staged) {  // the chain in place over the batch; culled rays (status NONE) are skipped
+      TraceJob job{};
+      job.rays = d_rays;
+      job.out_rays = d_rays;
+      job.status = d_st;
+      job.segments = d_seg;
+      job.alive_in = d_st;
+      job.n = m;
+      job.ld = B;
+      if (bzr_status s = run_fused<kModeStage>(ctx, set, job, flags)) return s;
+    } else {
+      for (uint32_t l = 0; l < nlens; ++l)
+        for (uint32_t j = 0; j < 2; ++j) {
+          Out o{};
+          o.rays = d_rays;
+          o.expected_all = j == 0 ? uint32_t(BZR_RR_INSIDE) : uint32_t(BZR_RR_OUTSIDE);
+          o.status = d_st;
+          o.segments = d_seg;
+          o.ri = set.lens[l].ri;
+          if (bzr_status s = run_segment<kModeStage>(use_fast(flags), ctx, set.lens[l], d_rays, B, 0, m, d_st, o, w)) return s;
+        }
+    }
     hipLaunchKernelGGL(k_land, dim3(grid_for(m)), dim3(kBlock), 0, ctx->stream, *tg, make_float4(pn.x, pn.y, pn.z, pc),
                        cell_u, cell_v, d_rays, B, m, d_st, d_hist, d_stats);
     BZR_HIP(hipGetLastError());

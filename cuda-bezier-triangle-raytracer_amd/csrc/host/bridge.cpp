@@ -4,6 +4,8 @@
 //   BezierTriangle::intersect  reference/bezierTriangle.cpp:123-195
 //   BezierMesh::intersect      reference/bezierMesh.cpp:206-227
 //   BezierLens::refract        reference/bezierLens.cpp:4-34
+#include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -16,7 +18,14 @@ void check(bzr_status s) {
   if (s != BZR_OK) throw std::runtime_error(std::string("libbzr: ") + bzr_last_error());
 }
 
-Context::Context(int device) { check(bzr_ctx_create(device, &mCtx)); }
+namespace {
+std::atomic<uint64_t> g_next_context_id{1};
+std::mutex g_device_cache;  // guards every BezierMesh::mDevices (meshes are shared read-only across threads)
+// The C ABI counts rays in uint32_t: larger host batches are issued in slices of at most this many rays.
+constexpr std::size_t kMaxBatch = std::size_t(1) << 30;
+}  // namespace
+
+Context::Context(int device) : mId(g_next_context_id.fetch_add(1)) { check(bzr_ctx_create(device, &mCtx)); }
 Context::~Context() { bzr_ctx_destroy(mCtx); }
 void Context::sync() const { check(bzr_sync(mCtx)); }
 
@@ -32,7 +41,7 @@ Context &defaultContext() {
 }
 
 struct DeviceMesh {
-  bzr_ctx *owner = nullptr;
+  uint64_t owner = 0;  // Context::id()
   bzr_mesh *mesh = nullptr;
   ~DeviceMesh() { bzr_mesh_destroy(mesh); }
 };
@@ -80,13 +89,17 @@ void traceChain(std::vector<BezierLens const *> const &lenses, Ray const *rays, 
     meshes.push_back(l->getMesh().device(c));
     ri.push_back(l->getRefractiveIndex());
   }
-  std::vector<float> in = raysToSoa(rays, n), out(6 * n);
-  std::vector<uint32_t> st(n);
-  check(bzr_trace_chain(c.get(), meshes.data(), ri.data(), static_cast<uint32_t>(meshes.size()), in.data(),
-                        static_cast<uint32_t>(n), out.data(), st.data(), outSegments, BZR_HOST_PTRS));
-  for (std::size_t i = 0; i < n; ++i) {
-    outRays[i] = soaToRay(out, n, i);
-    outStatus[i] = static_cast<RefractionResult>(st[i]);
+  for (std::size_t off = 0; off < n; off += kMaxBatch) {
+    const std::size_t m = std::min(kMaxBatch, n - off);
+    std::vector<float> in = raysToSoa(rays + off, m), out(6 * m);
+    std::vector<uint32_t> st(m);
+    check(bzr_trace_chain(c.get(), meshes.data(), ri.data(), static_cast<uint32_t>(meshes.size()), in.data(),
+                          static_cast<uint32_t>(m), out.data(), st.data(), outSegments ? outSegments + off : nullptr,
+                          BZR_HOST_PTRS));
+    for (std::size_t i = 0; i < m; ++i) {
+      outRays[off + i] = soaToRay(out, m, i);
+      outStatus[off + i] = static_cast<RefractionResult>(st[i]);
+    }
   }
 }
 
@@ -101,6 +114,7 @@ void traceChainTiled(std::vector<Context *> const &ctxs, std::vector<BezierLens 
     handles.push_back(c->get());
     for (auto const *l : lenses) meshes.push_back(l->getMesh().device(*c));
   }
+  if (n > UINT32_MAX) throw std::length_error("traceChainTiled: more than 2^32-1 rays in one call");
   std::vector<float> in = raysToSoa(rays, n), out(6 * n);
   std::vector<uint32_t> st(n);
   check(bzr_trace_tiled(handles.data(), static_cast<uint32_t>(handles.size()), meshes.data(), ri.data(),
@@ -115,10 +129,11 @@ void traceChainTiled(std::vector<Context *> const &ctxs, std::vector<BezierLens 
 }  // namespace bzr
 
 bzr_mesh *BezierMesh::device(bzr::Context &ctx) const {
+  std::lock_guard<std::mutex> lock(bzr::g_device_cache);
   for (auto const &dm : mDevices)
-    if (dm->owner == ctx.get()) return dm->mesh;
+    if (dm->owner == ctx.id()) return dm->mesh;
   auto dm = std::make_shared<bzr::DeviceMesh>();
-  dm->owner = ctx.get();
+  dm->owner = ctx.id();
   bzr::check(bzr_mesh_create(ctx.get(), mMesh.empty() ? nullptr : mMesh.data(), static_cast<uint32_t>(mMesh.size()),
                              sizeof(BezierTriangle), &dm->mesh));
   mDevices.push_back(dm);
@@ -128,11 +143,15 @@ bzr_mesh *BezierMesh::device(bzr::Context &ctx) const {
 void BezierMesh::intersect(Ray const *rays, std::size_t n, BezierIntersection *out, uint32_t *patchIndex,
                            bzr::Context *ctx) const {
   bzr::Context &c = ctx ? *ctx : bzr::defaultContext();
-  std::vector<float> in = bzr::raysToSoa(rays, n), hits(13 * n);
-  bzr::check(bzr_intersect(c.get(), device(c), in.data(), static_cast<uint32_t>(n), hits.data(), BZR_HOST_PTRS));
-  for (std::size_t i = 0; i < n; ++i) {
-    out[i] = bzr::hitFromSoa(hits, n, i);
-    if (patchIndex) std::memcpy(&patchIndex[i], &hits[12 * n + i], 4);
+  bzr_mesh *dm = device(c);
+  for (std::size_t off = 0; off < n; off += bzr::kMaxBatch) {
+    const std::size_t m = std::min(bzr::kMaxBatch, n - off);
+    std::vector<float> in = bzr::raysToSoa(rays + off, m), hits(13 * m);
+    bzr::check(bzr_intersect(c.get(), dm, in.data(), static_cast<uint32_t>(m), hits.data(), BZR_HOST_PTRS));
+    for (std::size_t i = 0; i < m; ++i) {
+      out[off + i] = bzr::hitFromSoa(hits, m, i);
+      if (patchIndex) std::memcpy(&patchIndex[off + i], &hits[12 * m + i], 4);
+    }
   }
 }
 
@@ -157,14 +176,18 @@ BezierIntersection BezierTriangle::intersect(Ray const &ray, LimitPlaneIntersect
 void BezierLens::refract(Ray const *rays, RefractionResult const *expected, std::size_t n, Ray *outRays,
                          RefractionResult *outStatus, bzr::Context *ctx) const {
   bzr::Context &c = ctx ? *ctx : bzr::defaultContext();
-  std::vector<float> in = bzr::raysToSoa(rays, n), out(6 * n);
-  std::vector<uint32_t> exp(n), st(n);
-  for (std::size_t i = 0; i < n; ++i) exp[i] = static_cast<uint32_t>(expected[i]);
-  bzr::check(bzr_refract(c.get(), mMesh.device(c), mRefractiveIndex, in.data(), exp.data(), 0u,
-                         static_cast<uint32_t>(n), out.data(), st.data(), BZR_HOST_PTRS));
-  for (std::size_t i = 0; i < n; ++i) {
-    outRays[i] = bzr::soaToRay(out, n, i);
-    outStatus[i] = static_cast<RefractionResult>(st[i]);
+  bzr_mesh *dm = mMesh.device(c);
+  for (std::size_t off = 0; off < n; off += bzr::kMaxBatch) {
+    const std::size_t m = std::min(bzr::kMaxBatch, n - off);
+    std::vector<float> in = bzr::raysToSoa(rays + off, m), out(6 * m);
+    std::vector<uint32_t> exp(m), st(m);
+    for (std::size_t i = 0; i < m; ++i) exp[i] = static_cast<uint32_t>(expected[off + i]);
+    bzr::check(bzr_refract(c.get(), dm, mRefractiveIndex, in.data(), exp.data(), 0u, static_cast<uint32_t>(m),
+                           out.data(), st.data(), BZR_HOST_PTRS));
+    for (std::size_t i = 0; i < m; ++i) {
+      outRays[off + i] = bzr::soaToRay(out, m, i);
+      outStatus[off + i] = static_cast<RefractionResult>(st[i]);
+    }
   }
 }
 

@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define BZR_ABI_VERSION 1
+#define BZR_ABI_VERSION 2
 
 typedef int32_t bzr_status;
 enum {
@@ -69,7 +69,16 @@ enum {
   BZR_DEVICE_PTRS = 1u,
   BZR_MODE_PARITY = 0u,
   BZR_MODE_FAST = 2u,
-  BZR_ACCEL_NONE = 4u   /* brute-force patch scan instead of the (bit-identical) BVH-culled path */
+  BZR_ACCEL_NONE = 4u,  /* brute-force patch scan instead of the (bit-identical) BVH-culled path */
+  /* Culled-path pipeline (same output bits either way; neither flag = automatic choice):
+   *   fused   one kernel per call (k_trace): each wave walks the BVH and runs the Newton stage for its own
+   *           rays with patch-uniform records -- no per-pair HBM traffic; best when a wave's rays meet
+   *           few distinct patches (dense ray grids: more than ~2000 rays per patch)
+   *   staged  traverse -> bucket pairs by patch -> Newton -> resolve -> finish per segment; full-wave
+   *           Newton passes whatever the ray coherence, at ~12x the algorithmic HBM bytes
+   * automatic: fused when n >= 2048 x the largest lens's patch count, else staged. */
+  BZR_PIPELINE_STAGED = 8u,
+  BZR_PIPELINE_FUSED = 16u
 };
 
 enum { BZR_WHAT_FOLLOW0 = 0, BZR_WHAT_FOLLOW1 = 1, BZR_WHAT_FOLLOW2 = 2, BZR_WHAT_NONE = 3, BZR_WHAT_INTERSECT = 4 };
@@ -103,7 +112,11 @@ bzr_status bzr_ctx_create(int32_t hip_device, bzr_ctx **out);
 bzr_status bzr_ctx_destroy(bzr_ctx *ctx);
 /* Launch on a caller-owned hipStream_t (NULL = the HIP null stream);
  * bzr_ctx_use_own_stream() goes back to the context's own non-blocking stream.  Work already queued
- * on the previous stream is ordered before later launches (an event hand-off, no host wait). */
+ * on the previous stream is ordered before later launches (an event hand-off, no host wait): the
+ * hand-off records an event on the previous stream, so a caller stream must stay alive while it is
+ * bound and until the next bzr_ctx_set_stream / bzr_ctx_use_own_stream / bzr_ctx_destroy returns.
+ * Device-pointer calls launch on the bound stream and return before the kernels finish: inputs must
+ * be ready on that stream, and outputs are valid on it (or after bzr_sync). */
 bzr_status bzr_ctx_set_stream(bzr_ctx *ctx, void *hip_stream);
 bzr_status bzr_ctx_use_own_stream(bzr_ctx *ctx);
 bzr_status bzr_ctx_get_stream(bzr_ctx *ctx, void **hip_stream);
@@ -122,7 +135,8 @@ enum {
   BZR_KERNEL_CHAIN_SCAN = 8,
   BZR_KERNEL_PATCH = 9,
   BZR_KERNEL_NEWTON_LANE = 10,    /* Newton stage for fragmented pair chunks, one patch record per lane */
-  BZR_KERNEL_COUNT = 11
+  BZR_KERNEL_TRACE = 11,          /* fused culled path: BVH walk + gate + Newton + winner (+ refraction chain) */
+  BZR_KERNEL_COUNT = 12
 };
 /* While enabled, every launch is bracketed by hipEvents on the context's stream. */
 bzr_status bzr_ctx_timing(bzr_ctx *ctx, int32_t enable);
@@ -136,8 +150,12 @@ enum {
   BZR_COUNTER_PAIRS = 1,         /* (ray, patch) pairs that passed the planar gate: Newton runs */
   BZR_COUNTER_FOLLOWS = 2,       /* follow-side retries on a neighbour patch: Newton runs */
   BZR_COUNTER_OVERFLOW_RAYS = 3, /* rays resolved by the in-order full scan */
-  BZR_COUNTER_LANE_CHUNKS = 4,   /* 64-pair chunks spanning many patches, run one record per lane */
-  BZR_COUNTER_COUNT = 5
+  BZR_COUNTER_LANE_CHUNKS = 4,   /* staged path: 64-pair chunks spanning many patches, one record per lane */
+  BZR_COUNTER_NODE_VISITS = 5,   /* fused path: BVH nodes fetched (per wave, 128 B each) */
+  BZR_COUNTER_LEAF_FETCHES = 6,  /* fused path: leaf gate records fetched (per wave, 64 B each) */
+  BZR_COUNTER_GATE_TESTS = 7,    /* fused path: planar gates evaluated (per ray: lanes whose box test hit a fetched leaf) */
+  BZR_COUNTER_NEWTON_ROUNDS = 8, /* fused path: patch-uniform Newton passes (per wave; cThis + follow-side) */
+  BZR_COUNTER_COUNT = 9
 };
 /* While enabled, each culled segment adds its counts on the device (one tiny kernel per segment). */
 bzr_status bzr_ctx_counters(bzr_ctx *ctx, int32_t enable);

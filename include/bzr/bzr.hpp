@@ -381,10 +381,13 @@ class Context {
   Context(Context const &) = delete;
   Context &operator=(Context const &) = delete;
   bzr_ctx *get() const { return mCtx; }
+  // Process-unique, never reused (a new Context may get a destroyed one's bzr_ctx address).
+  uint64_t id() const { return mId; }
   void sync() const;
 
  private:
   bzr_ctx *mCtx = nullptr;
+  uint64_t mId = 0;
 };
 void check(bzr_status s);  // throws std::runtime_error with bzr_last_error() text
 struct DeviceMesh;         // device copy of a patch array (bzr_mesh)
@@ -407,7 +410,7 @@ class BezierMesh final {
   // Batch interface (GPU).  patchIndex (optional) receives the index of the patch hit, ~0u on a miss.
   void intersect(Ray const *rays, std::size_t n, BezierIntersection *out, uint32_t *patchIndex = nullptr,
                  bzr::Context *ctx = nullptr) const;
-  // Device handle of this mesh on ctx (uploaded on first use and cached per context).
+  // Device handle of this mesh on ctx (uploaded on first use and cached per context; thread-safe).
   bzr_mesh *device(bzr::Context &ctx) const;
 
  private:

@@ -59,7 +59,29 @@ def lib():
     global _lib
     if _lib is None:
         build()
-        L = ctypes.CDLL(str(LIB_PATH))
+        _lib = _configure(ctypes.CDLL(str(LIB_PATH)))
+    return _lib
+
+
+def load_variant(cflags: str, tag: str):
+    """The oracle compiled with other flags (e.g. "-O3 -march=native" for bench.py's CPU baseline) into
+    a private temporary library; returns its configured handle.  Compiled where it runs (-march=native
+    must describe the host that times it)."""
+    import os
+    import tempfile
+
+    out = Path(tempfile.gettempdir()) / f"bzr_oracle_{tag}_{os.getuid()}_{os.getpid()}.so"
+    cmd = ["gcc", *cflags.split(), "-std=c11", "-fPIC", "-ffp-contract=off", "-fopenmp", "-shared", "-o", str(out),
+           str(ORACLE_DIR / "bzr_oracle.c"), str(ORACLE_DIR / "illum_oracle.c"), "-lm"]
+    subprocess.run(cmd, check=True, capture_output=True)
+    try:
+        return _configure(ctypes.CDLL(str(out)))
+    finally:
+        out.unlink(missing_ok=True)  # the mapping stays valid
+
+
+def _configure(L):
+    if True:
         sig = {
             "orc_last_error": ([], ctypes.c_char_p),
             "orc_mesh_init": ([_MP], None),
@@ -116,8 +138,7 @@ def lib():
             fn = getattr(L, name)
             fn.argtypes = args
             fn.restype = ret
-        _lib = L
-    return _lib
+    return L
 
 
 def v(x, y=None, z=None) -> ov3:
@@ -244,12 +265,12 @@ class OMesh:
 
 
 # ------------------------------------------------------------------ hot path
-def intersect(patches: np.ndarray, rays: np.ndarray, threads: int = 0) -> np.ndarray:
+def intersect(patches: np.ndarray, rays: np.ndarray, threads: int = 0, L=None) -> np.ndarray:
     p = np.ascontiguousarray(patches, dtype=np.float32)
     r = np.ascontiguousarray(rays, dtype=np.float32)
     n = r.shape[1]
     out = np.empty((13, n), np.float32)
-    lib().orc_intersect_batch(p.ctypes.data, len(p), r.ctypes.data, n, out.ctypes.data, threads)
+    (L or lib()).orc_intersect_batch(p.ctypes.data, len(p), r.ctypes.data, n, out.ctypes.data, threads)
     return out
 
 
@@ -282,7 +303,7 @@ def refract(patches, ri, rays, expected, threads=0):
     return o, s
 
 
-def trace_chain(lenses, ri, rays, threads=0):
+def trace_chain(lenses, ri, rays, threads=0, L=None):
     ps = [np.ascontiguousarray(p, dtype=np.float32) for p in lenses]
     ptrs = (ctypes.c_void_p * len(ps))(*[p.ctypes.data for p in ps])
     nps = (ctypes.c_uint32 * len(ps))(*[len(p) for p in ps])
@@ -292,7 +313,7 @@ def trace_chain(lenses, ri, rays, threads=0):
     o = np.empty((6, n), np.float32)
     s = np.empty(n, np.uint32)
     g = np.empty(n, np.uint32)
-    lib().orc_trace_chain_batch(ctypes.cast(ptrs, ctypes.c_void_p), ctypes.cast(nps, ctypes.c_void_p),
+    (L or lib()).orc_trace_chain_batch(ctypes.cast(ptrs, ctypes.c_void_p), ctypes.cast(nps, ctypes.c_void_p),
                                 ctypes.cast(ris, ctypes.c_void_p), len(ps), r.ctypes.data, n, o.ctypes.data,
                                 s.ctypes.data, g.ctypes.data, threads)
     return o, s, g

@@ -1,0 +1,16 @@
+#!/bin/bash
+# rocprofv3 passes over bench.py on the GPU box: kernel-trace stats, FETCH_SIZE, WRITE_SIZE and two SQ
+# counter sets, each in its own run (PMC passes with --kernel-trace only).  Output under gpurun_out/$TAG.
+# usage: TAG=name BENCH="--config cfg4 ..." bash scripts/prof_run.sh
+R="$GRAFT_REPO_ROOT"; OUT="$R/gpurun_out/${TAG:-prof}"; mkdir -p "$OUT"; cd /tmp && export TMPDIR=/tmp
+B="$R/bench.py --steps ${STEPS:-5} --warmup 1 --cpu-baseline off ${BENCH:-}"
+run() {  # run <name> <rocprof args...>
+  local name=$1; shift
+  timeout -k 10 300 rocprofv3 "$@" -d "$OUT/$name" -o run -- python3 $B > "$OUT/$name.log" 2>&1
+  local rc=$?; echo "$name rc=$rc" >> "$OUT/steps.txt"; return $rc
+}
+run trace --kernel-trace --stats &&
+run fetch --pmc FETCH_SIZE --kernel-trace &&
+run write --pmc WRITE_SIZE --kernel-trace &&
+run sq1 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU --kernel-trace &&
+run sq2 --pmc SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_SMEM SQ_INSTS_LDS SQ_LEVEL_WAVES --kernel-trace

@@ -49,3 +49,9 @@ def ctx(bzr):
     if n == 0:
         pytest.fail("GPU test on a machine without a HIP device (libbzr has no CPU path)")
     return bzr.Context(0)
+
+
+@pytest.fixture(params=["fused", "staged"])
+def pipe(request, bzr):
+    """The culled path's two pipelines (include/bzr.h BZR_PIPELINE_*): parity tests run both."""
+    return bzr.PIPELINE_FUSED if request.param == "fused" else bzr.PIPELINE_STAGED

@@ -30,7 +30,7 @@ def test_python_binding_covers_the_header(bzr):
 
 
 def test_abi_version_and_patch_layout(bzr):
-    assert bzr.lib().bzr_abi_version() == 1
+    assert bzr.lib().bzr_abi_version() == 2
     # bzr_patch is the reference's 264-byte BezierTriangle (reference/bezierTriangle.h:64-80)
     assert bzr.PATCH_WORDS * 4 == 264
 

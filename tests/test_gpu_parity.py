@@ -42,56 +42,56 @@ def meshes(bzr):
     return out
 
 
-def test_cfg1_full_grid_intersect(bzr, orc, ctx, meshes):
+def test_cfg1_full_grid_intersect(bzr, orc, ctx, meshes, pipe):
     cfg = CONFIGS["cfg1"]
     patches = meshes["cfg1"][0]
     rays = grid_rays(cfg)  # the full 256x256 config
-    got = bzr.intersect(ctx, bzr.DeviceMesh(ctx, patches), rays)
+    got = bzr.intersect(ctx, bzr.DeviceMesh(ctx, patches), rays, mode=pipe)
     want = orc.intersect(patches, rays)
     assert_hits_equal(got, want, "cfg1")
     assert abs((want.view(np.uint32)[11] == 4).mean() - 0.3433) < 5e-4  # 34.33 % hits
 
 
-def test_cfg2_chain_and_single_refracts(bzr, orc, ctx, meshes):
+def test_cfg2_chain_and_single_refracts(bzr, orc, ctx, meshes, pipe):
     cfg = CONFIGS["cfg2"]
     lens = meshes["cfg2"][0]
     rays = grid_rays(cfg, side=128)
     dm = bzr.DeviceMesh(ctx, lens)
-    o, s, g = bzr.trace_chain(ctx, [dm], [1.3], rays)
+    o, s, g = bzr.trace_chain(ctx, [dm], [1.3], rays, mode=pipe)
     wo, ws, wg = orc.trace_chain([lens], [1.3], rays)
     assert np.array_equal(s, ws) and np.array_equal(g, wg)
     assert np.array_equal(o.view(np.uint32), wo.view(np.uint32))
     # the same chain as two single refract() calls
     n = rays.shape[1]
-    o1, s1 = bzr.refract(ctx, dm, 1.3, rays, np.full(n, 1, np.uint32))
+    o1, s1 = bzr.refract(ctx, dm, 1.3, rays, np.full(n, 1, np.uint32), mode=pipe)
     w1, ws1 = orc.refract(lens, 1.3, rays, np.full(n, 1, np.uint32))
     assert np.array_equal(s1, ws1) and np.array_equal(o1.view(np.uint32), w1.view(np.uint32))
-    o2, s2 = bzr.refract(ctx, dm, 1.3, o1, None, expected_all=2)
+    o2, s2 = bzr.refract(ctx, dm, 1.3, o1, None, expected_all=2, mode=pipe)
     w2, ws2 = orc.refract(lens, 1.3, w1, np.full(n, 2, np.uint32))
     alive = ws1 != 0
     assert np.array_equal(s2[alive], ws2[alive])
     assert abs(g.mean() - 1.68) < 0.02  # 1.68 segments / primary
 
 
-def test_cfg4_two_lens_chain(bzr, orc, ctx, meshes):
+def test_cfg4_two_lens_chain(bzr, orc, ctx, meshes, pipe):
     cfg = CONFIGS["cfg4"]
     lenses = [build_lens(bzr.TriMesh, l).bezier_patches() for l in cfg.lenses]
     rays = grid_rays(cfg, side=96)
     dms = [bzr.DeviceMesh(ctx, p) for p in lenses]
-    o, s, g = bzr.trace_chain(ctx, dms, [1.3, 1.3], rays)
+    o, s, g = bzr.trace_chain(ctx, dms, [1.3, 1.3], rays, mode=pipe)
     wo, ws, wg = orc.trace_chain(lenses, [1.3, 1.3], rays)
     assert np.array_equal(s, ws) and np.array_equal(g, wg)
     assert np.array_equal(o.view(np.uint32), wo.view(np.uint32))
 
 
-def test_cfg3_robot_intersect(bzr, orc, ctx, meshes):
+def test_cfg3_robot_intersect(bzr, orc, ctx, meshes, pipe):
     cfg = CONFIGS["cfg3"]
     patches = meshes["cfg3"][0]
     assert len(patches) == 28800
     r, c = pixel_coords(cfg, side=2048)
     pick = np.random.default_rng(3).choice(len(r), 3000, replace=False)
     rays = rays_for(cfg, r[pick], c[pick], side=2048)
-    got = bzr.intersect(ctx, bzr.DeviceMesh(ctx, patches), rays)
+    got = bzr.intersect(ctx, bzr.DeviceMesh(ctx, patches), rays, mode=pipe)
     want = orc.intersect(patches, rays)
     assert_hits_equal(got, want, "cfg3")
 
@@ -118,7 +118,7 @@ def test_patch_intersect_aimed_rays(bzr, orc, ctx, meshes):
 
 
 @pytest.mark.parametrize("center", [0.0, 10.0])
-def test_seeded_cone_rays(bzr, orc, ctx, center):
+def test_seeded_cone_rays(bzr, orc, ctx, center, pipe):
     """SURVEY 8c fixture F4: 4096 rays, jittered origins on x=0, directions in a +-15 degree cone."""
     m = bzr.TriMesh().make_ellipsoid(32, 16, (1.0, 4.0, 2.0)).translate((center, 0.0, 0.0)).standardize()
     patches = m.bezier_patches()
@@ -130,12 +130,12 @@ def test_seeded_cone_rays(bzr, orc, ctx, center):
     th, ph = rng.uniform(0, ang, n), rng.uniform(0, 2 * np.pi, n)
     d = np.stack([np.cos(th), np.sin(th) * np.cos(ph), np.sin(th) * np.sin(ph)], 1).astype(np.float32)
     rays = np.concatenate([org.T, d.T]).astype(np.float32)
-    got = bzr.intersect(ctx, bzr.DeviceMesh(ctx, patches), rays)
+    got = bzr.intersect(ctx, bzr.DeviceMesh(ctx, patches), rays, mode=pipe)
     want = orc.intersect(patches, rays)
     assert_hits_equal(got, want, f"cone@{center}")
 
 
-def test_edge_cases(bzr, orc, ctx, meshes):
+def test_edge_cases(bzr, orc, ctx, meshes, pipe):
     patches = meshes["cfg1"][0]
     dm = bzr.DeviceMesh(ctx, patches)
     cfg = CONFIGS["cfg1"]
@@ -145,17 +145,17 @@ def test_edge_cases(bzr, orc, ctx, meshes):
     # ragged sizes around the 256-thread block
     for n in (1, 63, 255, 257, 1000):
         rays = grid_rays(cfg, side=64, order="rows")[:, :n].copy()
-        assert_hits_equal(bzr.intersect(ctx, dm, rays), orc.intersect(patches, rays), f"n={n}")
+        assert_hits_equal(bzr.intersect(ctx, dm, rays, mode=pipe), orc.intersect(patches, rays), f"n={n}")
     # empty mesh: every ray misses
     empty = bzr.DeviceMesh(ctx, np.zeros((0, 66), np.float32))
-    h = bzr.intersect(ctx, empty, grid_rays(cfg, side=16))
+    h = bzr.intersect(ctx, empty, grid_rays(cfg, side=16), mode=pipe)
     assert (h.view(np.uint32)[11] == 3).all() and (h[0] == np.finfo(np.float32).max).all()
     # degenerate directions: zero vector, grazing (parallel to x planes), backwards
     rays = np.zeros((6, 4), np.float32)
     rays[:, 1] = (-5, 0.1, 0.2, 0, 1, 0)
     rays[:, 2] = (-5, 0.1, 0.2, -1, 0, 0)
     rays[:, 3] = (0.0, 0.0, 0.0, 1, 0, 0)  # starts inside the sphere
-    assert_hits_equal(bzr.intersect(ctx, dm, rays), orc.intersect(patches, rays), "degenerate")
+    assert_hits_equal(bzr.intersect(ctx, dm, rays, mode=pipe), orc.intersect(patches, rays), "degenerate")
 
 
 def test_device_pointer_path_and_determinism(bzr, orc, ctx, meshes):
@@ -183,12 +183,12 @@ def test_device_pointer_path_and_determinism(bzr, orc, ctx, meshes):
 
 
 @pytest.mark.slow
-def test_cfg2_full_size_chain(bzr, orc, ctx, meshes):
+def test_cfg2_full_size_chain(bzr, orc, ctx, meshes, pipe):
     """BASELINE configs[1] at its full 1024x1024 size against the oracle (a few seconds of CPU)."""
     cfg = CONFIGS["cfg2"]
     lens = meshes["cfg2"][0]
     rays = grid_rays(cfg)
-    o, s, g = bzr.trace_chain(ctx, [bzr.DeviceMesh(ctx, lens)], [1.3], rays)
+    o, s, g = bzr.trace_chain(ctx, [bzr.DeviceMesh(ctx, lens)], [1.3], rays, mode=pipe)
     wo, ws, wg = orc.trace_chain([lens], [1.3], rays)
     assert np.array_equal(s, ws) and np.array_equal(g, wg)
     assert np.array_equal(o.view(np.uint32), wo.view(np.uint32))
@@ -232,22 +232,22 @@ def test_cfg4_full_size_properties(bzr, orc, ctx):
 
 
 # ---------------------------------------------------------------- culled == brute force
-def test_culled_equals_bruteforce_cfg2_full(bzr, ctx, meshes):
+def test_culled_equals_bruteforce_cfg2_full(bzr, ctx, meshes, pipe):
     """Default (BVH-culled) chain vs the brute-force scan over the full cfg2 image: every bit equal."""
     cfg = CONFIGS["cfg2"]
     dm = bzr.DeviceMesh(ctx, meshes["cfg2"][0])
     rays = grid_rays(cfg)
-    a = bzr.trace_chain(ctx, [dm], [1.3], rays)
+    a = bzr.trace_chain(ctx, [dm], [1.3], rays, mode=pipe)
     b = bzr.trace_chain(ctx, [dm], [1.3], rays, mode=bzr.ACCEL_NONE)
     for x, y in zip(a, b):
         assert np.array_equal(x.view(np.uint32), y.view(np.uint32))
 
 
-def test_culled_equals_bruteforce_robot_and_random(bzr, orc, ctx, meshes):
+def test_culled_equals_bruteforce_robot_and_random(bzr, orc, ctx, meshes, pipe):
     cfg = CONFIGS["cfg3"]
     dm = bzr.DeviceMesh(ctx, meshes["cfg3"][0])
     rays = grid_rays(cfg, side=512)
-    a = bzr.intersect(ctx, dm, rays)
+    a = bzr.intersect(ctx, dm, rays, mode=pipe)
     b = bzr.intersect(ctx, dm, rays, mode=bzr.ACCEL_NONE)
     assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
     # far origins on the robot mesh: every ray takes the overflow scan, which splits the 28800 patches
@@ -258,7 +258,7 @@ def test_culled_equals_bruteforce_robot_and_random(bzr, orc, ctx, meshes):
     o = tgt + rng.normal(size=(20000, 3)) * 1e4 * np.abs(hi - lo).max()
     d = (tgt - o) / np.linalg.norm(tgt - o, axis=1, keepdims=True)
     far = np.concatenate([o.T, d.T]).astype(np.float32)
-    a = bzr.intersect(ctx, dm, far)
+    a = bzr.intersect(ctx, dm, far, mode=pipe)
     b = bzr.intersect(ctx, dm, far, mode=bzr.ACCEL_NONE)
     assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
     assert (a.view(np.uint32)[11] == 4).mean() > 0.05
@@ -275,29 +275,29 @@ def test_culled_equals_bruteforce_robot_and_random(bzr, orc, ctx, meshes):
     o[far] *= 1e4  # beyond the culling radius: full-scan fallback
     rays = np.concatenate([o.T, d.T]).astype(np.float32)
     dm2 = bzr.DeviceMesh(ctx, meshes["cfg2"][0])
-    a = bzr.intersect(ctx, dm2, rays)
+    a = bzr.intersect(ctx, dm2, rays, mode=pipe)
     b = bzr.intersect(ctx, dm2, rays, mode=bzr.ACCEL_NONE)
     assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
     assert (a.view(np.uint32)[11] == 4).mean() > 0.1
-    o1, s1 = bzr.refract(ctx, dm2, 1.3, rays, None, expected_all=1)
+    o1, s1 = bzr.refract(ctx, dm2, 1.3, rays, None, expected_all=1, mode=pipe)
     o2, s2 = bzr.refract(ctx, dm2, 1.3, rays, None, expected_all=1, mode=bzr.ACCEL_NONE)
     assert np.array_equal(s1, s2) and np.array_equal(o1.view(np.uint32), o2.view(np.uint32))
 
 
 @pytest.mark.slow
-def test_cfg5_sample_against_oracle(bzr, orc, ctx):
+def test_cfg5_sample_against_oracle(bzr, orc, ctx, pipe):
     """cfg5 (301056 patches): a sample of its 8192^2 grid, culled GPU path vs the oracle."""
     cfg = CONFIGS["cfg5"]
     patches = build_lens(bzr.TriMesh, cfg.lenses[0]).bezier_patches()
     r, c = pixel_coords(cfg, side=8192, order="rows")
     pick = np.random.default_rng(5).choice(len(r), 384, replace=False)
     rays = rays_for(cfg, r[pick], c[pick], side=8192)
-    got = bzr.intersect(ctx, bzr.DeviceMesh(ctx, patches), rays)
+    got = bzr.intersect(ctx, bzr.DeviceMesh(ctx, patches), rays, mode=pipe)
     want = orc.intersect(patches, rays, threads=16)
     assert_hits_equal(got, want, "cfg5")
 
 
-def test_mixed_size_lenses_and_mesh_switching(bzr, orc, ctx, meshes):
+def test_mixed_size_lenses_and_mesh_switching(bzr, orc, ctx, meshes, pipe):
     """Lenses of different patch counts in one chain, and one context switching between meshes of
     different sizes (small-scan and hipCUB paths): every segment must start from zeroed counters and
     histogram whichever mesh ran before it."""
@@ -307,7 +307,7 @@ def test_mixed_size_lenses_and_mesh_switching(bzr, orc, ctx, meshes):
     rays = grid_rays(CONFIGS["cfg2"], side=96)
     dms = [bzr.DeviceMesh(ctx, p) for p in lenses]
     for order in ([0, 1], [1, 0]):
-        got = bzr.trace_chain(ctx, [dms[k] for k in order], [1.3, 1.5], rays)
+        got = bzr.trace_chain(ctx, [dms[k] for k in order], [1.3, 1.5], rays, mode=pipe)
         want = orc.trace_chain([lenses[k] for k in order], [1.3, 1.5], rays)
         for g, w in zip(got, want):
             assert np.array_equal(np.asarray(g).view(np.uint32), np.asarray(w).view(np.uint32))
@@ -317,5 +317,17 @@ def test_mixed_size_lenses_and_mesh_switching(bzr, orc, ctx, meshes):
     r3 = grid_rays(CONFIGS["cfg3"], side=32)
     for dm, p in seq:
         rr = r3 if dm is robot else rays[:, :2048]
-        got = bzr.intersect(ctx, dm, rr)
+        got = bzr.intersect(ctx, dm, rr, mode=pipe)
         assert np.array_equal(got.view(np.uint32), orc.intersect(p, rr).view(np.uint32))
+
+
+@pytest.mark.slow
+def test_culled_equals_bruteforce_cfg3_full(bzr, ctx, meshes, pipe):
+    """cfg3 (robot.stl x8 split, 28 800 patches) at its full 2048x2048 grid: culled == brute force, every bit."""
+    dm = bzr.DeviceMesh(ctx, meshes["cfg3"][0])
+    rays = grid_rays(CONFIGS["cfg3"])
+    assert rays.shape[1] == 2048 * 2048
+    a = bzr.intersect(ctx, dm, rays, mode=pipe)
+    b = bzr.intersect(ctx, dm, rays, mode=bzr.ACCEL_NONE)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    assert abs((a.view(np.uint32)[11] == 4).mean() - 0.2505) < 0.001  # 25.05 % of the 2048^2 grid (SURVEY 8d: 27.0 % on a 64^2 grid)

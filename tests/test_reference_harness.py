@@ -92,3 +92,91 @@ def test_product_matches_oracle_on_reference_harness(bzr, orc, ctx):
         assert (l1, j1, r1, s1) == (l2, j2, r2, s2)
         if s1:
             assert np.array_equal(o1.view(np.uint32), o2.view(np.uint32)), (l1, j1, r1)
+
+
+# ------------------------------------------------------------------ testBezierIntersection
+# reference/test.cpp:237-328, restated: the test lens (same envelope, test.cpp:241-245) is moved by +5 in x
+# and re-standardized in place before every step (test.cpp:260-264, the moves accumulate); each step
+# intersects the ray with the Bezier mesh, restarts the ray at the hit point (direction unchanged) and
+# intersects again (test.cpp:268-292); the loop ends at the first miss.  The harness prints
+# Ray::getAverageErrorSquared over the hit points plus one point 11 units past the last (test.cpp:317-319).
+# main() does not call it and the reference publishes no output for it, so its arguments here are ours;
+# the published pin is README.md:110's accuracy (distance from the ray / shape size, typically 3e-6, rare
+# cases 2e-4), which tests/test_reference_accuracy.py checks hit by hit.
+ISECT_CASES = [  # (sectors, belts, direction): every case crosses several lens copies before it misses
+    (21, 15, (1.0, -0.03, 0.04)),
+    (21, 15, (1.0, 0.1, 0.05)),
+    (32, 16, (1.0, 0.05, 0.02)),
+]
+ISECT_CAP = 60  # steps; a ray straight down the axis never leaves the lens copies
+
+
+def unit_dir(d):
+    """Ray(start, dir) normalises dir (3dGeomUtil.h:176-178) with Eigen's normalized()."""
+    f = np.float32
+    d = np.array(d, np.float32)
+    z = f(d[0] * d[0] + f(d[1] * d[1] + d[2] * d[2]))
+    return (d / np.sqrt(z)).astype(np.float32) if z > 0 else d
+
+
+def run_intersection_harness(mesh, intersect, sectors, direction):
+    """Drive test.cpp:254-293; `intersect(patches, rays [6, 1]) -> hits [13, 1]`.  Returns the event log
+    [(step, k, hit words)] and the hit points."""
+    d = unit_dir(direction)
+    s = np.zeros(3, np.float32)
+    log, points = [], []
+    for step in range(ISECT_CAP):
+        mesh.translate((5.0, 0.0, 0.0))
+        mesh.standardize_vertices()
+        mesh.standardize_normals()
+        patches = mesh.bezier_patches()
+        for k in range(2):
+            h = intersect(patches, np.concatenate([s, d]).astype(np.float32).reshape(6, 1))
+            log.append((step, k, h[:, 0].view(np.uint32).copy()))
+            if h.view(np.uint32)[11, 0] != 4:
+                return log, points
+            s = h[1:4, 0].copy()
+            points.append(s.copy())
+    return log, points
+
+
+def harness_error(orc, direction, points):
+    """Ray::getAverageErrorSquared (3dGeomUtil.h:199-205) of the original ray over the points plus the
+    point 11 units past the last one along the ray (test.cpp:318-319)."""
+    import ctypes
+
+    d = unit_dir(direction)
+    pts = list(points) + ([(points[-1] + d * np.float32(11.0)).astype(np.float32)] if points else [])
+    if not pts:
+        return 0.0
+    ray = orc.oray(orc.v(0.0, 0.0, 0.0), orc.v(*map(float, d)))
+    arr = np.ascontiguousarray(np.array(pts, np.float32).reshape(-1))
+    return float(orc.lib().orc_ray_average_error_squared(ctypes.byref(ray), arr.ctypes.data, len(pts)))
+
+
+@pytest.mark.parametrize("sectors,belts,direction", ISECT_CASES)
+def test_oracle_intersection_harness(orc, sectors, belts, direction):
+    mesh = orc.OMesh().make_solid_of_revolution(sectors, belts, 1, SIZE)
+    log, points = run_intersection_harness(mesh, lambda p, r: orc.intersect(p, r), sectors, direction)
+    assert 6 <= len(points) < 2 * ISECT_CAP  # enters and leaves several copies, then misses
+    err = harness_error(orc, direction, points)
+    # the printed error accumulates each restart's offset from the original ray; its RMS over the
+    # lens size stays within README.md:110's worst-case per-hit accuracy (2e-4)
+    assert np.sqrt(err) / 8.0 < 2e-4
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sectors,belts,direction", ISECT_CASES)
+def test_product_matches_oracle_on_intersection_harness(bzr, orc, ctx, pipe, sectors, belts, direction):
+    omesh = orc.OMesh().make_solid_of_revolution(sectors, belts, 1, SIZE)
+    olog, opts = run_intersection_harness(omesh, lambda p, r: orc.intersect(p, r), sectors, direction)
+
+    def gpu_intersect(patches, rays):
+        return bzr.intersect(ctx, bzr.DeviceMesh(ctx, patches), rays, mode=pipe)
+
+    pmesh = bzr.TriMesh().make_solid_of_revolution(sectors, belts, bzr.ENVELOPE_TESTLENS, SIZE)
+    plog, ppts = run_intersection_harness(pmesh, gpu_intersect, sectors, direction)
+    assert len(plog) == len(olog)
+    for (s1, k1, w1), (s2, k2, w2) in zip(plog, olog):
+        assert (s1, k1) == (s2, k2) and np.array_equal(w1, w2), (s1, k1)
+    assert harness_error(orc, direction, ppts) == harness_error(orc, direction, opts)
