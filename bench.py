@@ -213,8 +213,10 @@ def main():
     gather = world > 1 and a.gather == "rays"
     rows = frame.PACKED_ROWS if chain else 13
     # double-buffered frame gather: frame k's packed results travel to rank 0 (RCCL, its own stream)
-    # while frame k+1 is traced; a buffer is refilled only after its previous gather completed
-    packed = [torch.empty((rows, n), dtype=torch.float32, device=dev) for _ in range(2)] if gather else None
+    # while frame k+1 is traced; a buffer is refilled only after its previous gather completed.  Buffers
+    # hold the largest rank's share (strong scaling may deal one tile fewer to some ranks).
+    npad = frame.padded_count(world, side, height)
+    packed = [torch.zeros((rows, npad), dtype=torch.float32, device=dev) for _ in range(2)] if gather else None
     gather_lists = [[torch.empty_like(packed[0]) for _ in range(world)] if (gather and rank == 0) else None
                     for _ in range(2)]
     pending = [None, None]
@@ -236,7 +238,7 @@ def main():
             if chain:
                 frame.pack(out_rays, out_status, out_seg, packed[slot])
             else:
-                packed[slot].copy_(hits)
+                packed[slot][:, :n].copy_(hits)
             pending[slot] = frame.gather(packed[slot], world, rank, gather_list=gather_lists[slot], async_op=True)
         frames[0] += 1
 

@@ -3,7 +3,8 @@
 One process per GPU (torch.distributed; "nccl" = RCCL over xGMI on MI355X, "gloo" on CPU for tests).
 Rays are independent, so the only exchange is the final gather.  The image is
 `width` x `height` pixels; 64x64 tiles are dealt round-robin to ranks (configs.shard_pixels) so
-every rank gets a similar mix of lens-hitting and missing rays.  A rank's result for one frame is a
+every rank gets a similar mix of lens-hitting and missing rays.  Strong scaling keeps the image fixed as
+ranks are added (bench.py's default); weak scaling grows it with the rank count.  A rank's result for one frame is a
 packed [7, n] float32 tensor: the 6 ray rows, then one raw 32-bit word per ray holding the status
 (bits 0-7) and the segment count (bits 8-15): 28 bytes per primary ray cross xGMI.
 """
@@ -14,21 +15,31 @@ import numpy as np
 from .configs import Config, rays_for, shard_pixels
 
 PACKED_ROWS = 7
+TILE = 64  # pixels per tile side
 
 
 def rank_rays(cfg: Config, rank: int, world: int, width: int, height: int):
     """(rows, cols, rays [6, n]) of this rank's tiles."""
-    rows, cols = shard_pixels(cfg, rank, world, side=width, height=height)
+    rows, cols = shard_pixels(cfg, rank, world, side=width, height=height, block=TILE)
     return rows, cols, rays_for(cfg, rows, cols, side=width, height=height)
 
 
+def padded_count(world: int, width: int, height: int) -> int:
+    """Pixels per rank in the gather buffers: the largest rank's share (tiles are dealt round-robin, so a
+    fixed image whose tile count is not a multiple of `world` leaves some ranks one tile short)."""
+    tiles = (width // TILE) * (height // TILE)
+    return -(-tiles // world) * TILE * TILE
+
+
 def pack(out_rays, out_status, out_segments, packed):
-    """Write one frame's results into `packed` [7, n] (torch tensors, same device)."""
+    """Write one frame's results into the first n columns of `packed` [7, >= n] (torch tensors, same
+    device); the columns past n are padding (padded_count) and are not read by assemble()."""
     import torch
 
-    packed[:6].copy_(out_rays)
+    n = out_rays.shape[1]
+    packed[:6, :n].copy_(out_rays)
     word = out_status.to(torch.int32) | (out_segments.to(torch.int32) << 8)
-    packed[6].copy_(word.view(torch.float32))
+    packed[6, :n].copy_(word.view(torch.float32))
     return packed
 
 
@@ -53,8 +64,9 @@ def assemble(parts, cfg: Config, world: int, width: int, height: int):
     seg = np.zeros(height * width, np.uint32)
     for r, part in enumerate(parts):
         p = part.cpu().numpy() if hasattr(part, "cpu") else np.asarray(part)
-        rows, cols = shard_pixels(cfg, r, world, side=width, height=height)
+        rows, cols = shard_pixels(cfg, r, world, side=width, height=height, block=TILE)
         flat = rows * width + cols
+        p = p[:, :len(flat)]  # drop the padding
         rays[:, flat] = p[:6]
         word = np.ascontiguousarray(p[6]).view(np.uint32)
         status[flat] = word & 0xFF

@@ -115,6 +115,10 @@ struct Hit {
 #ifndef BZR_NEWTON_ITERS
 #define BZR_NEWTON_ITERS 4
 #endif
+// BZR_NEWTON_UNROLL (A/B knob, default 0): unroll the 4 Newton iterations.
+#ifndef BZR_NEWTON_UNROLL
+#define BZR_NEWTON_UNROLL 0
+#endif
 constexpr uint32_t kFollow2 = 2u, kNone = 3u, kIntersect = 4u;
 
 // Correctly rounded binary32 division and square root.  HIP compiles `/` and

@@ -991,8 +991,18 @@ struct TraceJob {
   uint32_t ld;               // row stride of rays / out_rays / hits (>= n)
 };
 
+// BZR_TRACE_WPE (A/B knob, default 0 = the compiler's choice): amdgpu_waves_per_eu lower bound for k_trace.
+#ifndef BZR_TRACE_WPE
+#define BZR_TRACE_WPE 0
+#endif
+#if BZR_TRACE_WPE
+#define BZR_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(BZR_TRACE_WPE)))
+#else
+#define BZR_TRACE_ATTR
+#endif
 template <int kMode, bool kFast, bool kCount>
-__global__ __launch_bounds__(kBlock) void k_trace(LensSet lenses, TraceJob job, unsigned long long *__restrict__ counters) {
+__global__ __launch_bounds__(kBlock) BZR_TRACE_ATTR void k_trace(LensSet lenses, TraceJob job,
+                                                                 unsigned long long *__restrict__ counters) {
   __shared__ TraceLds lds[kWaves];
   const uint32_t lane = threadIdx.x & 63u;
   TraceLds &L = lds[threadIdx.x >> 6];

@@ -37,6 +37,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--side", type=int, default=0, help="rays per image side (0 = the config's own)")
+    ap.add_argument("--pipeline", default="fused", choices=["fused", "staged", "auto"])
     a = ap.parse_args()
     import torch
 
@@ -44,6 +45,7 @@ def main():
     from bzr_amd.configs import CONFIGS, build_lens, grid_rays
 
     cfg = CONFIGS[a.config]
+    pflag = {"fused": bzr_amd.PIPELINE_FUSED, "staged": bzr_amd.PIPELINE_STAGED, "auto": 0}[a.pipeline]
     patches = [build_lens(bzr_amd.TriMesh, l).bezier_patches() for l in cfg.lenses]
     ris = (ctypes.c_float * len(patches))(*[l.ri for l in cfg.lenses])
     rays = torch.from_numpy(grid_rays(cfg, side=a.side) if a.side else grid_rays(cfg)).cuda()
@@ -72,7 +74,7 @@ def main():
             def step(h=h, ctx=ctx, marr=marr, out=out, st=st, sg=sg):
                 r = h.bzr_trace_chain(ctx, marr, ris, len(patches), ctypes.c_void_p(rays.data_ptr()), n,
                                       ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(st.data_ptr()),
-                                      ctypes.c_void_p(sg.data_ptr()), bzr_amd.DEVICE_PTRS)
+                                      ctypes.c_void_p(sg.data_ptr()), bzr_amd.DEVICE_PTRS | pflag)
                 assert r == 0, h.bzr_last_error()
         else:  # BezierMesh::intersect configs (cfg3, cfg5): one segment per ray
             out = torch.empty((13, n), dtype=torch.float32, device="cuda")
@@ -81,7 +83,7 @@ def main():
 
             def step(h=h, ctx=ctx, m=meshes[0], out=out):
                 r = h.bzr_intersect(ctx, m, ctypes.c_void_p(rays.data_ptr()), n, ctypes.c_void_p(out.data_ptr()),
-                                    bzr_amd.DEVICE_PTRS)
+                                    bzr_amd.DEVICE_PTRS | pflag)
                 assert r == 0, h.bzr_last_error()
         for _ in range(3):
             step()
@@ -118,7 +120,7 @@ def main():
     segs = int(ref["sg"].sum().item())
     for r in runs:  # work counters of one frame
         h, ctx = r["h"], r["ctx"]
-        cnt = (ctypes.c_uint64 * 8)()
+        cnt = (ctypes.c_uint64 * 16)()
         h.bzr_ctx_counters(ctx, 1)
         h.bzr_ctx_counters_report(ctx, cnt)
         r["step"]()

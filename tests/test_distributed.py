@@ -29,7 +29,7 @@ def worker(rank, world, port, width, height, patches, result_path):
         cfg = CONFIGS["cfg2"]
         rows, cols, rays = frame.rank_rays(cfg, rank, world, width, height)
         o, s, g = pyoracle.trace_chain([patches], [1.3], rays, threads=2)
-        packed = torch.empty((frame.PACKED_ROWS, rays.shape[1]), dtype=torch.float32)
+        packed = torch.zeros((frame.PACKED_ROWS, frame.padded_count(world, width, height)), dtype=torch.float32)
         frame.pack(torch.from_numpy(o), torch.from_numpy(s.view(np.int32)), torch.from_numpy(g.view(np.int32)), packed)
         glist = [torch.empty_like(packed) for _ in range(world)] if rank == 0 else None
         parts = frame.gather(packed, world, rank, gather_list=glist)
@@ -40,11 +40,13 @@ def worker(rank, world, port, width, height, patches, result_path):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_frame_equals_single_process(bzr, orc, world, tmp_path):
+@pytest.mark.parametrize("world,scaling", [(2, "weak"), (3, "weak"), (2, "strong"), (3, "strong")])
+def test_sharded_frame_equals_single_process(bzr, orc, world, scaling, tmp_path):
+    """weak: the image grows with the ranks (128 x 64*world); strong (bench.py's default): a fixed 128x128
+    image dealt to the ranks -- at world 3 its 4 tiles split 2/1/1, so the gather buffers are padded."""
     cfg = CONFIGS["cfg2"]
     patches = bzr.TriMesh().make_ellipsoid(32, 16, (1, 4, 2)).translate((10, 0, 0)).standardize().bezier_patches()
-    width, height = 128, 64 * world
+    width, height = (128, 64 * world) if scaling == "weak" else (128, 128)
     out = tmp_path / "frame.npz"
     mp.start_processes(worker, args=(world, free_port(), width, height, patches, str(out)), nprocs=world,
                        join=True, start_method="spawn")
