@@ -115,9 +115,9 @@ struct Hit {
 #ifndef BZR_NEWTON_ITERS
 #define BZR_NEWTON_ITERS 4
 #endif
-// BZR_NEWTON_UNROLL (A/B knob, default 0): unroll the 4 Newton iterations.
+// BZR_NEWTON_UNROLL (default 1): unroll the 4 Newton iterations (+1.7 % fused cfg4, +0.7 % staged cfg2/cfg3).
 #ifndef BZR_NEWTON_UNROLL
-#define BZR_NEWTON_UNROLL 0
+#define BZR_NEWTON_UNROLL 1
 #endif
 constexpr uint32_t kFollow2 = 2u, kNone = 3u, kIntersect = 4u;
 

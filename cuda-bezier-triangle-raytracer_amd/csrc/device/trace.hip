@@ -827,10 +827,19 @@ struct TraceCtr {  // wave-uniform work counters (kCount)
   uint32_t nodes = 0, leaves = 0, gate_tests = 0, rounds = 0, pairs = 0, follows = 0, segments = 0, ovf = 0;
 };
 constexpr int kHitWords = 12;  // t, point, cos, bary, normal, source patch
+// BZR_TRACE_LDS_RECORD (A/B knob, default 0): the Newton site reads the patch record from a per-wave LDS
+// copy (volatile per-use ds_reads) instead of SGPRs -- the operand path a per-lane-record pass would use.
+#ifndef BZR_TRACE_LDS_RECORD
+#define BZR_TRACE_LDS_RECORD 0
+#endif
 struct TraceLds {              // per wave
   uint32_t stack[kStack];
   float hit[kHitWords][64];    // the lane's current winner (written only when it improves)
+#if BZR_TRACE_LDS_RECORD
+  float rec[2][rec::kWords];
+#endif
 };
+typedef __attribute__((address_space(3))) const volatile float lds_vfloat;
 
 __device__ __forceinline__ uint32_t popc64(unsigned long long m) { return (uint32_t)__popcll(m); }
 
@@ -959,7 +968,12 @@ __device__ __forceinline__ void trace_segment(const MeshView &m, f3 s, f3 d, boo
         if (lim) ctr.follows += popc64(__ballot(run));
         else ctr.pairs += popc64(__ballot(run));
       }
+#if BZR_TRACE_LDS_RECORD
+      for (uint32_t k = lane; k < (uint32_t)rec::kWords; k += 64u) L.rec[0][k] = m.full[(size_t)rec::kWords * pb + k];
+      const PatchView<lds_vfloat *> pa{(lds_vfloat *)&L.rec[0][0]};
+#else
       const auto pa = uniform_patch(m.full, pb);
+#endif
       if (run) {
         const Hit h = patch_intersect<false, kFast>(pa, s, d, lim);
         consider(h, b, pb, best, L, lane);

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Throughput of the other BASELINE.json configs on 1 GPU (bench.py measures cfg2): one JSON line each.
+"""Throughput of the BASELINE.json configs on 1 GPU (bench.py measures cfg4): one JSON line each.
 
 cfg3: robot.stl split x8 (28800 patches), 2048^2 primary rays, BezierMesh::intersect.
 cfg4: two cfg2 lenses, 4096^2 rays, refraction chain (BASELINE quotes it on 8 GPUs; here 1 GPU's share
@@ -7,7 +7,7 @@ cfg4: two cfg2 lenses, 4096^2 rays, refraction chain (BASELINE quotes it on 8 GP
 cfg5: 301056-patch ellipsoid, BezierMesh::intersect; 4096^2 of its 8192^2 grid (one quarter: the full
       grid is 8 GPUs' work, 2x one rank's share).
 Inputs resident in HBM; K timed repetitions after one warm-up; Mrays/s counts BezierMesh::intersect calls.
-usage: bench_configs.py [cfg3 cfg4 cfg5] [--fast]   (--fast: BZR_MODE_FAST)
+usage: bench_configs.py [cfg2 cfg3 cfg4 cfg5] [--fast] [--pipeline fused|staged|auto]
 """
 import json
 import sys
@@ -72,7 +72,9 @@ def run(name, side, reps, mode=bzr_amd.MODE_PARITY):
     extra = {"kernels_ms": kern, "counters": cnt}
     if g is None:
         extra["hit_fraction"] = round(float((hits[11].view(torch.int32) == 4).float().mean().item()), 4)
-    print(json.dumps({"config": name, "mode": "fast" if mode & bzr_amd.MODE_FAST else "parity", "rays_side": side, "patches": int(sum(len(p) for p in patches)),
+    pipe = "fused" if mode & bzr_amd.PIPELINE_FUSED else "staged" if mode & bzr_amd.PIPELINE_STAGED else "auto"
+    print(json.dumps({"config": name, "mode": "fast" if mode & bzr_amd.MODE_FAST else "parity", "pipeline": pipe,
+                      "rays_side": side, "patches": int(sum(len(p) for p in patches)),
                       "segments_per_step": segs, "ms_per_step": round(dt * 1e3, 3),
                       "mrays_per_s": round(segs / dt / 1e6, 1), "preprocess_s": round(prep, 2),
                       "upload_bvh_s": round(upload, 2), **extra}), flush=True)
@@ -83,8 +85,14 @@ def run(name, side, reps, mode=bzr_amd.MODE_PARITY):
 def main():
     args = sys.argv[1:]
     mode = bzr_amd.MODE_FAST if "--fast" in args else bzr_amd.MODE_PARITY
-    which = [a for a in args if not a.startswith("--")] or ["cfg3", "cfg4", "cfg5"]
-    plan = {"cfg3": (2048, 10), "cfg4": (4096, 5), "cfg5": (4096, 3)}
+    pipeline = "auto"
+    if "--pipeline" in args:
+        pipeline = args[args.index("--pipeline") + 1]
+        args.remove("--pipeline")
+        args.remove(pipeline)
+    mode |= {"fused": bzr_amd.PIPELINE_FUSED, "staged": bzr_amd.PIPELINE_STAGED, "auto": 0}[pipeline]
+    which = [a for a in args if not a.startswith("--")] or ["cfg2", "cfg3", "cfg4", "cfg5"]
+    plan = {"cfg2": (1024, 20), "cfg3": (2048, 10), "cfg4": (4096, 5), "cfg5": (8192, 3)}
     for name in which:
         run(name, *plan[name], mode=mode)
 

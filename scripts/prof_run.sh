@@ -1,7 +1,9 @@
 #!/bin/bash
 # rocprofv3 passes over bench.py on the GPU box: kernel-trace stats, FETCH_SIZE, WRITE_SIZE and two SQ
 # counter sets, each in its own run (PMC passes with --kernel-trace only).  Output under gpurun_out/$TAG.
-# usage: TAG=name BENCH="--config cfg4 ..." bash scripts/prof_run.sh
+# usage: TAG=name BENCH="--config cfg4 ..." [WORKLOAD=cfg4/fused/parity/4096] bash scripts/prof_run.sh
+# The rocprofv3 databases are summarised on the box (scripts/prof_summary.py -> $TAG/summary.txt and
+# $TAG/pmc_traffic.json) and then deleted, so the pulled gpurun_out/ stays small.
 R="$GRAFT_REPO_ROOT"; OUT="$R/gpurun_out/${TAG:-prof}"; mkdir -p "$OUT"; cd /tmp && export TMPDIR=/tmp
 B="$R/bench.py --steps ${STEPS:-5} --warmup 1 --cpu-baseline off ${BENCH:-}"
 run() {  # run <name> <rocprof args...>
@@ -13,4 +15,7 @@ run trace --kernel-trace --stats &&
 run fetch --pmc FETCH_SIZE --kernel-trace &&
 run write --pmc WRITE_SIZE --kernel-trace &&
 run sq1 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU --kernel-trace &&
-run sq2 --pmc SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_SMEM SQ_INSTS_LDS SQ_LEVEL_WAVES --kernel-trace
+run sq2 --pmc SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_SMEM SQ_INSTS_LDS SQ_LEVEL_WAVES --kernel-trace &&
+timeout -k 10 120 python3 "$R/scripts/prof_summary.py" "$OUT" "$OUT/summary.txt" --note "rocprofv3 over bench.py ${BENCH:-} (steps ${STEPS:-5})" \
+  --traffic-json "$OUT/pmc_traffic.json" --workload "${WORKLOAD:-$TAG}" > /dev/null &&
+find "$OUT" -name "*.db" -delete

@@ -2,6 +2,7 @@
 """Summarise a scripts/prof_run.sh output directory (rocprofv3 databases) into a text file.
 
 usage: prof_summary.py <run dir> <out.txt> [--note TEXT] [--traffic-json profiles/pmc_traffic.json --workload KEY]
+       prof_summary.py --merge <box pmc_traffic.json> profiles/pmc_traffic.json
 
 Sections: the kernel-trace stats (calls, total, average per launch, resources), then per kernel the PMC
 counters averaged over launches with derived ratios:
@@ -121,7 +122,18 @@ def write_traffic(p, source, out, workload):
     print(f"wrote {out}: {workload}: {len(kern)} kernels")
 
 
+def merge(src, dst):
+    """Merge the workloads of a box-side pmc_traffic.json into the committed one."""
+    d = json.loads(Path(dst).read_text()) if Path(dst).exists() else {"unit": "HBM bytes per launch"}
+    d.setdefault("workloads", {}).update(json.loads(Path(src).read_text())["workloads"])
+    Path(dst).write_text(json.dumps(d, indent=1) + "\n")
+
+
 def main():
+    import sys
+    if len(sys.argv) == 4 and sys.argv[1] == "--merge":
+        merge(sys.argv[2], sys.argv[3])
+        return
     ap = argparse.ArgumentParser()
     ap.add_argument("rundir")
     ap.add_argument("out")
