@@ -66,6 +66,8 @@ struct bzr_mesh {
   float4 *leaf;     // 4 float4 per BVH leaf slot: the planar record, patch index in the last word
   bzr_host::Bvh4Node *nodes_near;  // the near tier's tree and leaf slots (bvh.hpp kTierNear)
   float4 *leaf_near;
+  bzr_host::Bvh4ObbNode *obb;       // both tiers' wide-patch subtrees (oriented boxes, bvh.hpp)
+  bzr_host::Bvh4ObbNode *obb_near;
   uint32_t nnodes;
   float s_max;      // far tier: origins beyond take the full scan
   float s_near;     // near tier: waves whose rays all start within it walk the tighter tree
@@ -156,6 +158,8 @@ struct MeshView {
   const float4 *__restrict__ leaf;
   const bzr_host::Bvh4Node *__restrict__ nodes_near;
   const float4 *__restrict__ leaf_near;
+  const bzr_host::Bvh4ObbNode *__restrict__ obb;
+  const bzr_host::Bvh4ObbNode *__restrict__ obb_near;
   uint32_t n;
   float s_max;
   float s_near;
@@ -311,6 +315,56 @@ __device__ __forceinline__ bool slab(float4 lo, float4 hi, f3 s, f3 sinv, f3 inv
   return tnear <= tfar && tfar >= 0.0f;
 }
 
+// Ray vs oriented box (bvh.hpp Bvh4ObbNode): the slab test in the box's frame.  Culling only (no parity
+// requirement): FMA and v_rcp_f32 are fine, their error is inside the box's doubled padding (bvh.cpp).
+__device__ __forceinline__ float clamped_rcp(float x) {
+  return __builtin_amdgcn_rcpf(fabsf(x) < 1e-20f ? copysignf(1e-20f, x) : x);
+}
+// q: one child's 64-byte record (bvh.hpp Bvh4ObbChild)
+__device__ __forceinline__ bool obb_hit(const u32x16 &q, f3 s, f3 d) {
+  const float rx = s.x - __uint_as_float(q[0]), ry = s.y - __uint_as_float(q[1]), rz = s.z - __uint_as_float(q[2]);
+  float tnear = -FLT_MAX, tfar = FLT_MAX;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    const float ux = __uint_as_float(q[3 + 3 * a]), uy = __uint_as_float(q[4 + 3 * a]), uz = __uint_as_float(q[5 + 3 * a]);
+    const float o = __builtin_fmaf(rx, ux, __builtin_fmaf(ry, uy, rz * uz));
+    const float dd = __builtin_fmaf(d.x, ux, __builtin_fmaf(d.y, uy, d.z * uz));
+    const float h = __uint_as_float(q[12 + a]), inv = clamped_rcp(dd);
+    const float t1 = (-h - o) * inv, t2 = (h - o) * inv;
+    tnear = fmaxf(tnear, fminf(t1, t2));
+    tfar = fminf(tfar, fmaxf(t1, t2));
+  }
+  return tnear <= tfar && tfar >= 0.0f;
+}
+
+// The children of BVH node `ref` (an AABB node, or an oriented-box node when ref has kObbFlag): their
+// refs and which lanes' rays hit their boxes (wave-uniform fetch: two or four 64-byte scalar loads).
+__device__ __forceinline__ void node_children(const bzr_host::Bvh4Node *nodes, const bzr_host::Bvh4ObbNode *obb,
+                                              uint32_t ref, bool act, f3 s, f3 d, f3 sinv, f3 inv, bool (&hit)[4],
+                                              uint32_t (&ch)[4]) {
+  if (ref & bzr_host::kObbFlag) {  // one 64-byte scalar load per child (16 SGPRs live at a time)
+    const cu32x16 *np = (const cu32x16 *)(uintptr_t)(obb + (ref & ~bzr_host::kObbFlag));
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const u32x16 q = np[c];
+      ch[c] = q[15];
+      hit[c] = act & (ch[c] != bzr_host::kEmptyChild) & obb_hit(q, s, d);
+    }
+    return;
+  }
+  // the whole 128-byte node in two 64-byte scalar loads and one wait (all words used unconditionally)
+  const cu32x16 *np = (const cu32x16 *)(uintptr_t)(nodes + ref);
+  const u32x16 na = np[0], nb = np[1];
+  // words: lo.x[0..3] lo.y lo.z hi.x | hi.y hi.z child[0..3] pad
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const float4 lo = make_float4(__uint_as_float(na[c]), __uint_as_float(na[4 + c]), __uint_as_float(na[8 + c]), 0.0f);
+    const float4 hi = make_float4(__uint_as_float(na[12 + c]), __uint_as_float(nb[c]), __uint_as_float(nb[4 + c]), 0.0f);
+    ch[c] = nb[8 + c];
+    hit[c] = act & (ch[c] != bzr_host::kEmptyChild) & slab(lo, hi, s, sinv, inv);
+  }
+}
+
 // Per-segment pipeline of the culled path (one BezierMesh::intersect per ray of a chunk of n rays;
 // external arrays -- rays, alive, outputs -- are indexed off + i with row stride ld):
 //   k_traverse  BVH walk, exact planar gate -> up to kMaxCand candidates per ray, a per-patch
@@ -420,6 +474,7 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
   const bool far_ray = active && !(fmaxf(fmaxf(fabsf(s.x), fabsf(s.y)), fabsf(s.z)) <= m.s_near);
   const bool near_tier = !__any(far_ray);
   const bzr_host::Bvh4Node *nodes = near_tier ? m.nodes_near : m.nodes;
+  const bzr_host::Bvh4ObbNode *obb = near_tier ? m.obb_near : m.obb;
   const float4 *leaf = near_tier ? m.leaf_near : m.leaf;
   const f3 inv = mk(safe_inv(d.x), safe_inv(d.y), safe_inv(d.z));
   const f3 sinv = mk(s.x * inv.x, s.y * inv.y, s.z * inv.z);
@@ -430,19 +485,9 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
   }
   while (sp > 0) {
     const uint32_t node = __builtin_amdgcn_readfirstlane(stk[--sp]);
-    // the whole 128-byte node in two 64-byte scalar loads and one wait (all words used unconditionally)
-    const cu32x16 *np = (const cu32x16 *)(uintptr_t)(nodes + node);
-    const u32x16 na = np[0], nb = np[1];
-    // words: lo.x[0..3] lo.y lo.z hi.x | hi.y hi.z child[0..3] pad
     bool hit[4];
     uint32_t ch[4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const float4 lo = make_float4(__uint_as_float(na[c]), __uint_as_float(na[4 + c]), __uint_as_float(na[8 + c]), 0.0f);
-      const float4 hi = make_float4(__uint_as_float(na[12 + c]), __uint_as_float(nb[c]), __uint_as_float(nb[4 + c]), 0.0f);
-      ch[c] = nb[8 + c];
-      hit[c] = active & (ch[c] != bzr_host::kEmptyChild) & slab(lo, hi, s, sinv, inv);
-    }
+    node_children(nodes, obb, node, active, s, d, sinv, inv, hit, ch);
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       if (!__any(hit[c])) continue;
@@ -879,6 +924,7 @@ __device__ __forceinline__ void trace_segment(const MeshView &m, f3 s, f3 d, boo
   }
   const bool near_tier = !__any(act && !(amax <= m.s_near));
   const bzr_host::Bvh4Node *nodes = near_tier ? m.nodes_near : m.nodes;
+  const bzr_host::Bvh4ObbNode *obb = near_tier ? m.obb_near : m.obb;
   const float4 *leaf = near_tier ? m.leaf_near : m.leaf;
   const f3 inv = mk(safe_inv(d.x), safe_inv(d.y), safe_inv(d.z));
   const f3 sinv = mk(s.x * inv.x, s.y * inv.y, s.z * inv.z);
@@ -895,18 +941,10 @@ __device__ __forceinline__ void trace_segment(const MeshView &m, f3 s, f3 d, boo
     if (qn == 0) {
       if (sp > 0) {
         const uint32_t node = __builtin_amdgcn_readfirstlane(L.stack[--sp]);
-        const cu32x16 *np = (const cu32x16 *)(uintptr_t)(nodes + node);
-        const u32x16 na = np[0], nb = np[1];
         if (kCount) ++ctr.nodes;
         bool hit[4];
         uint32_t ch[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const float4 lo = make_float4(__uint_as_float(na[c]), __uint_as_float(na[4 + c]), __uint_as_float(na[8 + c]), 0.0f);
-          const float4 hi = make_float4(__uint_as_float(na[12 + c]), __uint_as_float(nb[c]), __uint_as_float(nb[4 + c]), 0.0f);
-          ch[c] = nb[8 + c];
-          hit[c] = act & (ch[c] != bzr_host::kEmptyChild) & slab(lo, hi, s, sinv, inv);
-        }
+        node_children(nodes, obb, node, act, s, d, sinv, inv, hit, ch);
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
           const unsigned long long hm = __ballot(hit[c]);
@@ -1181,7 +1219,8 @@ struct DeviceGuard {
 };
 
 MeshView view_of(const bzr_mesh *m, float ri = 1.0f) {
-  return MeshView{m->planar, m->full, m->nodes, m->leaf, m->nodes_near, m->leaf_near, m->n, m->s_max, m->s_near, ri};
+  return MeshView{m->planar, m->full, m->nodes, m->leaf, m->nodes_near, m->leaf_near, m->obb, m->obb_near,
+                  m->n, m->s_max, m->s_near, ri};
 }
 unsigned grid_for(uint32_t n) { return (n + kBlock - 1) / kBlock; }
 size_t round256(size_t b) { return (b + 255) & ~size_t(255); }
@@ -1619,6 +1658,9 @@ extern "C" bzr_status bzr_mesh_create(bzr_ctx *ctx, const void *patches, uint32_
       {reinterpret_cast<void **>(&mesh->nodes_near), bvh_near.nodes4.data(),
        bvh_near.nodes4.size() * sizeof(bzr_host::Bvh4Node)},
       {reinterpret_cast<void **>(&mesh->leaf_near), leaf_near.data(), leaf_near.size() * sizeof(float4)},
+      {reinterpret_cast<void **>(&mesh->obb), bvh.obb.data(), bvh.obb.size() * sizeof(bzr_host::Bvh4ObbNode)},
+      {reinterpret_cast<void **>(&mesh->obb_near), bvh_near.obb.data(),
+       bvh_near.obb.size() * sizeof(bzr_host::Bvh4ObbNode)},
   };
   hipError_t e = hipSuccess;
   for (auto &u : ups) {
@@ -1645,6 +1687,8 @@ extern "C" bzr_status bzr_mesh_destroy(bzr_mesh *mesh) {
   (void)hipFree(mesh->leaf);
   (void)hipFree(mesh->nodes_near);
   (void)hipFree(mesh->leaf_near);
+  (void)hipFree(mesh->obb);
+  (void)hipFree(mesh->obb_near);
   delete mesh;
   return BZR_OK;
 }

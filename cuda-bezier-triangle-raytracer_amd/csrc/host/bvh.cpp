@@ -14,6 +14,7 @@
 #include "bvh.hpp"
 
 #include <algorithm>
+#include <cfloat>
 #include <array>
 #include <cmath>
 #include <cstring>
@@ -29,7 +30,21 @@ double dotd(d3 a, d3 b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
 d3 crossd(d3 a, d3 b) { return {a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]}; }
 double normd(d3 a) { return std::sqrt(dotd(a, a)); }
 
-constexpr double kRel = 1.0 / (1 << 18);  // rounding slack factor (~32x the float gate's unit error)
+// Rounding allowances of the float planar gate (u = 2^-24; X bounds |x| over the region, s_max |origin|):
+//   kRel    the plane slab eps and the ray-point / slab-test pad: the float ray/plane point p lies within
+//           ~18 u (X + s_max) of the plane (fl(n.s), fl(d.n) and the division's rounding, the last scaled
+//           by t: off-plane distance ~ t * err(d.n) <= 3 sqrt3 u |p - s|) -- 2^-18 = 64 u is 3.5x that
+//   kSlack  the barycentric slack: fl(M_i . p) differs from M_i . p by at most gamma_3 sum_j |M_ij p_j|
+//           <= 3.0000002 u l1_i X -- 2^-21 = 8 u is 2.7x that.  (Ill-conditioned M makes l1 large: this
+//           term sets the in-plane size of the wide patches' regions.)
+#ifndef BZR_BVH_KREL_LOG2
+#define BZR_BVH_KREL_LOG2 18
+#endif
+#ifndef BZR_BVH_KSLACK_LOG2
+#define BZR_BVH_KSLACK_LOG2 21
+#endif
+constexpr double kRel = 1.0 / (1 << BZR_BVH_KREL_LOG2);
+constexpr double kSlack = 1.0 / (1 << BZR_BVH_KSLACK_LOG2);
 
 // Clip convex polygon `poly` (plane points) to { x : g.x + h >= 0 }.
 std::vector<d3> clip(std::vector<d3> const &poly, d3 g, double h) {
@@ -52,7 +67,14 @@ std::vector<d3> clip(std::vector<d3> const &poly, d3 g, double h) {
 // ray/plane point, within eps of the plane and within pad of the ray.  So the region is the
 // parallelepiped P = { x : -slack <= M_i x <= 1 + slack } cut by the slab |n.x - c| <= eps:
 // its AABB is spanned by the two slab-face slices of P and the vertices of P inside the slab.
-Box gate_region_box(const float *rec, double s_max) {
+struct Region {       // the gate region's extreme points (double) and the ray-point padding
+  enum Kind { kEmpty, kFinite, kUnbounded };
+  Kind kind = kUnbounded;  // kEmpty: never a candidate; kUnbounded: non-finite record data
+  std::vector<d3> pts;
+  double pad = 0.0;
+};
+
+Box gate_region_box(const float *rec, double s_max, Region *region = nullptr) {
   d3 n{rec[0], rec[1], rec[2]};
   double c = rec[3];
   const float *m = rec + 49;  // col-major
@@ -90,40 +112,58 @@ Box gate_region_box(const float *rec, double s_max) {
   }
   if (!std::isfinite(ext)) return all;
   double X = ext;  // bound on |x| over P (every vertex of P is within sum |q_k| (1 + 2 slack))
+  // kappa = gamma_3 max_i l1_i sum_k |q_k|_inf (gamma_3 = 3.0000002 u, u = 2^-24): a passing float p has
+  // fl(M_i p) in [0,1], so |b_k| = |M_k p| <= 1 + gamma_3 l1 |p|_inf and |p|_inf <= sum_k |q_k|_inf |b_k|;
+  // for kappa < 1/2 that gives |p|_inf <= 2 sum_k |q_k| <= X, and slack_i = kSlack (l1_i X + 1) >=
+  // gamma_3 l1_i X is a proven allowance.  For kappa >= 1/2 the float gate's rounding is not bounded this
+  // way (the rows of M are nearly parallel to the normal: fl(M p) is rounding noise near the plane,
+  // SURVEY.md 0.4); those patches keep round 1's construction and allowance (kRel), and their culling
+  // is checked empirically (tests/test_gpu_parity.py culled == brute force).
+  double l1max = 0.0, qsum = 0.0;
+  for (int i = 0; i < 3; ++i) l1max = std::max(l1max, std::fabs(row[i][0]) + std::fabs(row[i][1]) + std::fabs(row[i][2]));
+  for (int k = 0; k < 3; ++k) qsum += std::max({std::fabs(q[k][0]), std::fabs(q[k][1]), std::fabs(q[k][2])});
+  const double kappa = 3.0000002 / 16777216.0 * l1max * qsum;
+  const double kslack = kappa < 0.5 ? kSlack : kRel;
   double slack[3];
   for (int i = 0; i < 3; ++i) {
     double l1 = std::fabs(row[i][0]) + std::fabs(row[i][1]) + std::fabs(row[i][2]);
-    slack[i] = kRel * (l1 * X + 1.0);
+    slack[i] = kslack * (l1 * X + 1.0);
   }
-  double eps = kRel * (X + s_max);  // off-plane distance of the float plane point
-  d3 lo{HUGE_VAL, HUGE_VAL, HUGE_VAL}, hi{-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
-  bool any = false;
-  auto take = [&](d3 const &p) {
-    any = true;
-    for (int a = 0; a < 3; ++a) {
-      lo[a] = std::min(lo[a], p[a]);
-      hi[a] = std::max(hi[a], p[a]);
-    }
-  };
+  const double eps = kRel * (X + s_max);  // off-plane distance of the float plane point
+  std::vector<d3> pts;
+  // the initial square must contain the whole slab slice of the slack-inflated parallelepiped
+  double qn = 0.0, smax_slack = std::max({slack[0], slack[1], slack[2]});
+  for (int k = 0; k < 3; ++k) qn += normd(q[k]);
+  const double e = 2.0 * (qn * (1.0 + 2.0 * smax_slack) + std::fabs(cu) + eps);
   for (double off : {-eps, eps}) {
     d3 x0 = {nu[0] * (cu + off), nu[1] * (cu + off), nu[2] * (cu + off)};
-    double e = 2.0 * (ext + std::fabs(cu) + eps);
-    std::vector<d3> region = {addm(addm(x0, u, -e), v, -e), addm(addm(x0, u, e), v, -e),
-                              addm(addm(x0, u, e), v, e), addm(addm(x0, u, -e), v, e)};
-    for (int i = 0; i < 3 && !region.empty(); ++i) {
-      region = clip(region, row[i], slack[i]);                                                   // M_i x >= -slack
-      if (!region.empty()) region = clip(region, {-row[i][0], -row[i][1], -row[i][2]}, 1.0 + slack[i]);  // <= 1+slack
+    std::vector<d3> poly = {addm(addm(x0, u, -e), v, -e), addm(addm(x0, u, e), v, -e),
+                            addm(addm(x0, u, e), v, e), addm(addm(x0, u, -e), v, e)};
+    for (int i = 0; i < 3 && !poly.empty(); ++i) {
+      poly = clip(poly, row[i], slack[i]);                                                   // M_i x >= -slack
+      if (!poly.empty()) poly = clip(poly, {-row[i][0], -row[i][1], -row[i][2]}, 1.0 + slack[i]);  // <= 1+slack
     }
-    for (auto const &p : region) take(p);
+    pts.insert(pts.end(), poly.begin(), poly.end());
   }
   for (int corner = 0; corner < 8; ++corner) {
     d3 b;
     for (int k = 0; k < 3; ++k) b[k] = (corner >> k) & 1 ? 1.0 + slack[k] : -slack[k];
     d3 p{0, 0, 0};
     for (int k = 0; k < 3; ++k) p = addm(p, q[k], b[k]);
-    if (std::fabs(dotd(nu, p) - cu) <= eps) take(p);
+    if (std::fabs(dotd(nu, p) - cu) <= eps) pts.push_back(p);
+  }
+  d3 lo{HUGE_VAL, HUGE_VAL, HUGE_VAL}, hi{-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
+  bool any = false;
+  for (auto const &p : pts) {
+    any = true;
+    if (region) region->pts.push_back(p);
+    for (int a = 0; a < 3; ++a) {
+      lo[a] = std::min(lo[a], p[a]);
+      hi[a] = std::max(hi[a], p[a]);
+    }
   }
   Box bx;
+  if (region) region->kind = any ? Region::kFinite : Region::kEmpty;
   if (!any) {  // no point of the slab passes the gate even with slack: never a candidate
     bx.lo = {1.0f, 1.0f, 1.0f};
     bx.hi = {0.0f, 0.0f, 0.0f};
@@ -131,6 +171,7 @@ Box gate_region_box(const float *rec, double s_max) {
     return bx;
   }
   double pad = kRel * (X + s_max) + 1e-6;  // ray-point and slab-test rounding
+  if (region) region->pad = pad;
   for (int a = 0; a < 3; ++a) {
     bx.lo[a] = static_cast<float>(std::nextafter(lo[a] - pad, -HUGE_VAL));
     bx.hi[a] = static_cast<float>(std::nextafter(hi[a] + pad, HUGE_VAL));
@@ -280,15 +321,193 @@ struct Builder {
 
 bool box_empty(BvhNode const &nd) { return !(nd.lo[0] <= nd.hi[0] && nd.lo[1] <= nd.hi[1] && nd.lo[2] <= nd.hi[2]); }
 
+// Eigenvectors of a symmetric 3x3 matrix (cyclic Jacobi), columns of v, by decreasing eigenvalue.
+void eigen_sym3(double a[3][3], double v[3][3]) {
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) v[i][j] = i == j ? 1.0 : 0.0;
+  for (int sweep = 0; sweep < 32; ++sweep) {
+    double off = std::fabs(a[0][1]) + std::fabs(a[0][2]) + std::fabs(a[1][2]);
+    if (!(off > 1e-300)) break;
+    for (int p = 0; p < 2; ++p)
+      for (int q = p + 1; q < 3; ++q) {
+        if (std::fabs(a[p][q]) < 1e-300) continue;
+        const double th = 0.5 * std::atan2(2.0 * a[p][q], a[q][q] - a[p][p]);
+        const double c = std::cos(th), sn = std::sin(th);
+        for (int k = 0; k < 3; ++k) {  // A <- J^T A J
+          const double akp = a[k][p], akq = a[k][q];
+          a[k][p] = c * akp - sn * akq;
+          a[k][q] = sn * akp + c * akq;
+        }
+        for (int k = 0; k < 3; ++k) {
+          const double apk = a[p][k], aqk = a[q][k];
+          a[p][k] = c * apk - sn * aqk;
+          a[q][k] = sn * apk + c * aqk;
+        }
+        for (int k = 0; k < 3; ++k) {
+          const double vkp = v[k][p], vkq = v[k][q];
+          v[k][p] = c * vkp - sn * vkq;
+          v[k][q] = sn * vkp + c * vkq;
+        }
+      }
+  }
+  int ord[3] = {0, 1, 2};
+  std::sort(ord, ord + 3, [&](int x, int y) { return a[x][x] > a[y][y]; });
+  double w[3][3];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) w[i][j] = v[i][ord[j]];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) v[i][j] = w[i][j];
+}
+
+// Oriented box (15 floats: c, u, v, w, h) enclosing `pts` inflated by `pad` on every axis.  The axes are
+// the points' principal directions, rounded to float; the centre and half extents are computed in double
+// against the ROUNDED axes, then widened by `pad` and rounded outward, so the float box contains every
+// point in exact arithmetic; the device test's own float error is covered by the pad (bvh.cpp header).
+bool fit_obb(std::vector<d3> const &pts, double pad, float out[15]) {
+  // the "always hit" box for regions without a finite description (non-finite records: full scan semantics)
+  for (int k = 0; k < 15; ++k) out[k] = 0.0f;
+  out[3] = out[7] = out[11] = 1.0f;
+  out[12] = out[13] = out[14] = HUGE_VALF;
+  if (pts.empty()) return false;
+  for (auto const &p : pts)
+    if (!std::isfinite(p[0]) || !std::isfinite(p[1]) || !std::isfinite(p[2])) return false;
+  d3 mean{0, 0, 0};
+  for (auto const &p : pts)
+    for (int k = 0; k < 3; ++k) mean[k] += p[k];
+  for (int k = 0; k < 3; ++k) mean[k] /= (double)pts.size();
+  double cov[3][3] = {};
+  for (auto const &p : pts)
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) cov[i][j] += (p[i] - mean[i]) * (p[j] - mean[j]);
+  double ev[3][3];
+  eigen_sym3(cov, ev);
+  float ax[3][3];
+  d3 u{ev[0][0], ev[1][0], ev[2][0]}, w{ev[0][2], ev[1][2], ev[2][2]};
+  double un = normd(u);
+  if (!(un > 0) || !std::isfinite(un)) return false;
+  u = {u[0] / un, u[1] / un, u[2] / un};
+  w = sub(w, {u[0] * dotd(w, u), u[1] * dotd(w, u), u[2] * dotd(w, u)});
+  double wn = normd(w);
+  if (!(wn > 1e-12)) {  // degenerate spread: any axis perpendicular to u
+    d3 helper = std::fabs(u[0]) < 0.6 ? d3{1, 0, 0} : d3{0, 1, 0};
+    w = crossd(u, helper);
+    wn = normd(w);
+  }
+  w = {w[0] / wn, w[1] / wn, w[2] / wn};
+  d3 v = crossd(w, u);
+  const d3 axes[3] = {u, v, w};
+  for (int a = 0; a < 3; ++a)
+    for (int k = 0; k < 3; ++k) ax[a][k] = static_cast<float>(axes[a][k]);
+  for (int a = 0; a < 3; ++a) {
+    double lo = HUGE_VAL, hi = -HUGE_VAL;
+    for (auto const &p : pts) {
+      const double t = p[0] * ax[a][0] + p[1] * ax[a][1] + p[2] * ax[a][2];
+      lo = std::min(lo, t);
+      hi = std::max(hi, t);
+    }
+    if (!std::isfinite(lo) || !std::isfinite(hi)) return false;
+    (void)lo;
+  }
+  // centre = mean rounded to float; half extents from the rounded centre along the rounded axes
+  float c[3];
+  for (int k = 0; k < 3; ++k) c[k] = static_cast<float>(mean[k]);
+  float h[3];
+  for (int a = 0; a < 3; ++a) {
+    double m = 0.0;
+    for (auto const &p : pts) {
+      const double t = (p[0] - c[0]) * ax[a][0] + (p[1] - c[1]) * ax[a][1] + (p[2] - c[2]) * ax[a][2];
+      m = std::max(m, std::fabs(t));
+    }
+    h[a] = static_cast<float>(std::nextafter(m + pad, HUGE_VAL));
+    if (!std::isfinite(h[a])) return false;
+  }
+  for (int k = 0; k < 3; ++k) out[k] = c[k];
+  for (int a = 0; a < 3; ++a)
+    for (int k = 0; k < 3; ++k) out[3 + 3 * a + k] = ax[a][k];
+  for (int a = 0; a < 3; ++a) out[12 + a] = h[a];
+  return true;
+}
+
 double half_area(BvhNode const &nd) {
   double e[3];
   for (int a = 0; a < 3; ++a) e[a] = std::max(0.0, (double)nd.hi[a] - (double)nd.lo[a]);
   return e[0] * e[1] + e[1] * e[2] + e[2] * e[0];
 }
 
+// Oriented boxes of the wide subtree: binary nodes [wide_first, ...) belong to it (the builder appends
+// them after the narrow subtree's); each covers order[range] and its box encloses the gate-region points
+// of those patches.
+struct ObbBuild {
+  uint32_t wide_first = 0xFFFFFFFFu;              // binary nodes from here on are in the wide subtree
+  uint32_t max_obb_patches = 4;                   // only nodes over at most this many patches get oriented boxes
+  std::vector<std::pair<uint32_t, uint32_t>> range;  // per binary node: (first, count) of order[]
+  std::vector<Region> const *region = nullptr;       // per patch (mesh order)
+  std::vector<uint32_t> const *order = nullptr;
+  std::vector<Bvh4ObbNode> *obb = nullptr;
+  bool obb_of(uint32_t n2, float out[15]) const {
+    std::vector<d3> pts;
+    double pad = 0.0;
+    for (uint32_t k = range[n2].first; k < range[n2].first + range[n2].second; ++k) {
+      Region const &r = (*region)[(*order)[k]];
+      if (r.kind == Region::kEmpty) continue;  // never a candidate
+      if (r.kind == Region::kUnbounded) {      // no finite gate region: cannot bound it
+        fit_obb({}, 0.0, out);
+        return false;
+      }
+      pts.insert(pts.end(), r.pts.begin(), r.pts.end());
+      pad = std::max(pad, r.pad);
+    }
+    return fit_obb(pts, 2.0 * pad, out);  // 2x: the rotated slab test's own rounding (header)
+  }
+};
+
+std::pair<uint32_t, uint32_t> fill_ranges(std::vector<BvhNode> const &bin, uint32_t n2,
+                                          std::vector<std::pair<uint32_t, uint32_t>> &range) {
+  if (bin[n2].b & kLeafFlag) return range[n2] = {bin[n2].a, bin[n2].b & ~kLeafFlag};
+  const auto l = fill_ranges(bin, bin[n2].a, range), r = fill_ranges(bin, bin[n2].b, range);
+  return range[n2] = {std::min(l.first, r.first), l.second + r.second};
+}
+
 // Collapse the binary tree under `n2` into 4-wide nodes: repeatedly open the child with the largest
 // box until four children remain.  Subtrees with empty boxes (no patch whose gate can pass) drop out.
-uint32_t collapse(std::vector<BvhNode> const &bin, uint32_t n2, std::vector<Bvh4Node> &out) {
+// Nodes of the wide subtree become Bvh4ObbNode (ref kObbFlag | index).
+uint32_t collapse(std::vector<BvhNode> const &bin, uint32_t n2, std::vector<Bvh4Node> &out, ObbBuild const &ob) {
+  if (n2 >= ob.wide_first && !(bin[n2].b & kLeafFlag) && ob.range[n2].second <= ob.max_obb_patches) {
+    std::vector<uint32_t> kids = {bin[n2].a, bin[n2].b};
+    while (kids.size() < 4) {
+      int best = -1;
+      double area = -1.0;
+      for (int i = 0; i < (int)kids.size(); ++i) {
+        BvhNode const &k = bin[kids[i]];
+        if ((k.b & kLeafFlag) || box_empty(k)) continue;
+        double ar = half_area(k);
+        if (ar > area || std::isnan(ar)) {
+          area = ar;
+          best = i;
+        }
+      }
+      if (best < 0) break;
+      uint32_t x = kids[best];
+      kids.erase(kids.begin() + best);
+      kids.push_back(bin[x].a);
+      kids.push_back(bin[x].b);
+    }
+    const uint32_t id = static_cast<uint32_t>(ob.obb->size());
+    ob.obb->push_back({});
+    Bvh4ObbNode nd{};
+    for (int c = 0; c < 4; ++c) {
+      nd.c[c].child = kEmptyChild;
+      fit_obb({}, 0.0, nd.c[c].f);  // (unused slots: never tested, their ref is empty)
+    }
+    for (int c = 0; c < (int)kids.size(); ++c) {
+      BvhNode const &k = bin[kids[c]];
+      if (box_empty(k)) continue;
+      ob.obb_of(kids[c], nd.c[c].f);  // on failure: the always-hit box
+      nd.c[c].child = (k.b & kLeafFlag) ? (kLeafFlag | k.a) : collapse(bin, kids[c], out, ob);
+    }
+    (*ob.obb)[id] = nd;
+    return kObbFlag | id;
+  }
   uint32_t id = static_cast<uint32_t>(out.size());
   out.push_back({});
   std::vector<uint32_t> kids;
@@ -323,7 +542,7 @@ uint32_t collapse(std::vector<BvhNode> const &bin, uint32_t n2, std::vector<Bvh4
       nd.lo[a][c] = k.lo[a];
       nd.hi[a][c] = k.hi[a];
     }
-    nd.child[c] = (k.b & kLeafFlag) ? (kLeafFlag | k.a) : collapse(bin, kids[c], out);
+    nd.child[c] = (k.b & kLeafFlag) ? (kLeafFlag | k.a) : collapse(bin, kids[c], out, ob);
   }
   out[id] = nd;
   return id;
@@ -351,8 +570,9 @@ Bvh build_bvh(const float *records, uint32_t n, uint32_t stride_words, int tier)
     }
   out.s_max = static_cast<float>(tier == kTierNear ? std::max(1.0, 8.0 * span) : std::max(1e3, 100.0 * span));
   out.extent = 0.0f;
+  std::vector<Region> region(n);
   for (uint32_t i = 0; i < n; ++i) {
-    box[i] = gate_region_box(records + (size_t)i * stride_words, out.s_max);
+    box[i] = gate_region_box(records + (size_t)i * stride_words, out.s_max, &region[i]);
     for (int a = 0; a < 3; ++a) {
       float lo = box[i].lo[a], hi = box[i].hi[a];
       bld.centre[i][a] = box[i].empty ? 0.0f : (std::isfinite(lo) && std::isfinite(hi) ? 0.5f * (lo + hi) : 0.0f);
@@ -383,9 +603,22 @@ Bvh build_bvh(const float *records, uint32_t n, uint32_t stride_words, int tier)
     auto mid = std::stable_partition(out.order.begin(), out.order.end(), [&](uint32_t i) { return !wide(i); });
     n_narrow = static_cast<uint32_t>(mid - out.order.begin());
   }
+  ObbBuild ob;
   if (n && n_narrow > 0 && n_narrow < n) {
     out.nodes.push_back({});  // root, filled below
-    const uint32_t l = bld.build(0, n_narrow), r = bld.build(n_narrow, n - n_narrow);
+    const uint32_t l = bld.build(0, n_narrow);
+// BZR_BVH_OBB (A/B knob, default 0): oriented boxes for the wide subtree (nodes over at most
+// BZR_BVH_OBB_MAX patches).  Measured on cfg5 (8192^2, staged): k_traverse 34.6 ms with them vs 24.4 ms
+// without -- fewer node and leaf visits (host replay 86 + 63 vs 97 + 105 per wave) but a 256-byte node
+// costs four dependent scalar loads within the SGPR budget, where an AABB node costs one.
+#ifndef BZR_BVH_OBB
+#define BZR_BVH_OBB 0
+#endif
+    if (BZR_BVH_OBB) ob.wide_first = static_cast<uint32_t>(out.nodes.size());
+#ifdef BZR_BVH_OBB_MAX
+    ob.max_obb_patches = BZR_BVH_OBB_MAX;
+#endif
+    const uint32_t r = bld.build(n_narrow, n - n_narrow);
     BvhNode root;
     for (int a = 0; a < 3; ++a) {
       root.lo[a] = std::min(out.nodes[l].lo[a], out.nodes[r].lo[a]);
@@ -398,7 +631,12 @@ Bvh build_bvh(const float *records, uint32_t n, uint32_t stride_words, int tier)
     bld.build(0, n);
   }
   if (n) {
-    collapse(out.nodes, 0, out.nodes4);
+    ob.range.resize(out.nodes.size());
+    fill_ranges(out.nodes, 0, ob.range);
+    ob.region = &region;
+    ob.order = &out.order;
+    ob.obb = &out.obb;
+    collapse(out.nodes, 0, out.nodes4, ob);
   } else {
     Bvh4Node root{};
     for (int c = 0; c < 4; ++c) root.child[c] = kEmptyChild;
@@ -411,6 +649,14 @@ Bvh build_bvh(const float *records, uint32_t n, uint32_t stride_words, int tier)
     d[0] = b.lo[0]; d[1] = b.lo[1]; d[2] = b.lo[2]; d[3] = 0.0f;
     d[4] = b.hi[0]; d[5] = b.hi[1]; d[6] = b.hi[2]; d[7] = 0.0f;
   }
+  out.patch_obb.assign((size_t)n * 16, 0.0f);
+  if (ob.wide_first != 0xFFFFFFFFu)
+    for (uint32_t k = n_narrow; k < n; ++k) {  // the wide patches' own boxes (what their parents test)
+      const uint32_t p = out.order[k];
+      if (region[p].kind == Region::kEmpty) continue;
+      fit_obb(region[p].pts, 2.0 * region[p].pad, &out.patch_obb[(size_t)p * 16]);  // always-hit if unbounded
+      out.patch_obb[(size_t)p * 16 + 15] = 1.0f;
+    }
   ritter_sphere(box, out.sphere);
   return out;
 }
@@ -499,6 +745,34 @@ bool slab_h(const float lo[3], const float hi[3], const float s[3], const float 
 }
 }  // namespace
 
+namespace {
+// host mirror of the device obb_hit (trace.hip; 1/x where the device uses v_rcp_f32: statistics only)
+bool obb_h(const float f[15], const float s[3], const float d[3]) {
+  const float r[3] = {s[0] - f[0], s[1] - f[1], s[2] - f[2]};
+  float tnear = -FLT_MAX, tfar = FLT_MAX;
+  for (int a = 0; a < 3; ++a) {
+    const float *u = f + 3 + 3 * a;
+    const float o = std::fma(r[0], u[0], std::fma(r[1], u[1], r[2] * u[2]));
+    const float dd = std::fma(d[0], u[0], std::fma(d[1], u[1], d[2] * u[2]));
+    const float inv = 1.0f / (std::fabs(dd) < 1e-20f ? std::copysign(1e-20f, dd) : dd);
+    const float h = f[12 + a], t1 = (-h - o) * inv, t2 = (h - o) * inv;
+    tnear = std::fmax(tnear, std::fmin(t1, t2));
+    tfar = std::fmin(tfar, std::fmax(t1, t2));
+  }
+  return tnear <= tfar && tfar >= 0.0f;
+}
+}  // namespace
+
+// Per patch (mesh order): its oriented gate-region box (c, u, v, w, h) and a flag word 1.0f when the patch
+// is in the wide subtree (the box its parent node tests), else 16 zeros.
+extern "C" int32_t bzr_debug_gate_obbs(const void *patches, uint32_t n, uint32_t stride, int32_t tier, float *out) {
+  if ((!patches && n) || (!out && n) || stride % 4 || stride < 264) return 1;
+  if (tier != bzr_host::kTierFar && tier != bzr_host::kTierNear) return 1;
+  bzr_host::Bvh bvh = bzr_host::build_bvh(static_cast<const float *>(patches), n, stride / 4, tier);
+  std::memcpy(out, bvh.patch_obb.data(), (size_t)n * 16 * sizeof(float));
+  return 0;
+}
+
 extern "C" int32_t bzr_debug_traverse(const void *patches, uint32_t n, uint32_t stride, const float *rays, uint32_t nr,
                                       uint8_t *hits, uint64_t stats[4]) {
   if ((!patches && n) || (!rays && nr) || !stats || stride % 4 || stride < 264) return 1;
@@ -507,13 +781,14 @@ extern "C" int32_t bzr_debug_traverse(const void *patches, uint32_t n, uint32_t 
   for (int k = 0; k < 4; ++k) stats[k] = 0;
   for (uint32_t w0 = 0; w0 < nr; w0 += 64) {
     uint32_t lanes = std::min<uint32_t>(64, nr - w0);
-    float s[64][3], inv[64][3];
+    float s[64][3], d[64][3], inv[64][3];
     bool active[64];
     for (uint32_t l = 0; l < lanes; ++l) {
       uint32_t r = w0 + l;
       for (int k = 0; k < 3; ++k) {
         s[l][k] = rays[(size_t)k * nr + r];
-        inv[l][k] = safe_inv_h(rays[(size_t)(3 + k) * nr + r]);
+        d[l][k] = rays[(size_t)(3 + k) * nr + r];
+        inv[l][k] = safe_inv_h(d[l][k]);
       }
       active[l] = std::fmax(std::fmax(std::fabs(s[l][0]), std::fabs(s[l][1])), std::fabs(s[l][2])) <= far.s_max;
     }
@@ -528,16 +803,23 @@ extern "C" int32_t bzr_debug_traverse(const void *patches, uint32_t n, uint32_t 
       uint32_t node = stack.back();
       stack.pop_back();
       stats[0] += 1;
-      bzr_host::Bvh4Node const &nd = bvh.nodes4[node];
+      const bool is_obb = node & bzr_host::kObbFlag;
+      bzr_host::Bvh4Node const *nd = is_obb ? nullptr : &bvh.nodes4[node];
+      bzr_host::Bvh4ObbNode const *od = is_obb ? &bvh.obb[node & ~bzr_host::kObbFlag] : nullptr;
       for (int c = 0; c < 4; ++c) {
-        if (nd.child[c] == bzr_host::kEmptyChild) continue;
-        float lo[3] = {nd.lo[0][c], nd.lo[1][c], nd.lo[2][c]}, hi[3] = {nd.hi[0][c], nd.hi[1][c], nd.hi[2][c]};
+        const uint32_t child = is_obb ? od->c[c].child : nd->child[c];
+        if (child == bzr_host::kEmptyChild) continue;
         bool any = false;
         bool hit[64];
-        for (uint32_t l = 0; l < lanes; ++l) any |= (hit[l] = active[l] && slab_h(lo, hi, s[l], inv[l]));
+        if (is_obb) {
+          for (uint32_t l = 0; l < lanes; ++l) any |= (hit[l] = active[l] && obb_h(od->c[c].f, s[l], d[l]));
+        } else {
+          float lo[3] = {nd->lo[0][c], nd->lo[1][c], nd->lo[2][c]}, hi[3] = {nd->hi[0][c], nd->hi[1][c], nd->hi[2][c]};
+          for (uint32_t l = 0; l < lanes; ++l) any |= (hit[l] = active[l] && slab_h(lo, hi, s[l], inv[l]));
+        }
         if (!any) continue;
-        if (nd.child[c] & bzr_host::kLeafFlag) {
-          uint32_t b = bvh.order[nd.child[c] & ~bzr_host::kLeafFlag];
+        if (child & bzr_host::kLeafFlag) {
+          uint32_t b = bvh.order[child & ~bzr_host::kLeafFlag];
           stats[1] += 1;
           for (uint32_t l = 0; l < lanes; ++l)
             if (hit[l]) {
@@ -545,7 +827,7 @@ extern "C" int32_t bzr_debug_traverse(const void *patches, uint32_t n, uint32_t 
               if (hits) hits[(size_t)(w0 + l) * n + b] = 1;
             }
         } else {
-          stack.push_back(nd.child[c]);
+          stack.push_back(child);
         }
       }
     }

@@ -33,8 +33,26 @@ struct Bvh4Node {
 };
 static_assert(sizeof(Bvh4Node) == 128, "Bvh4Node layout");
 
+// 4-wide node of the wide-patch subtree (256 bytes, read with four 64-byte scalar loads): each child is
+// bounded by an oriented box -- centre c, orthonormal axes u v w, half extents h -- instead of an AABB.
+// The wide patches' gate regions are long thin needles in planes through (nearly) the origin (SURVEY.md
+// 0.4): their AABBs span the scene, their oriented boxes do not.  One 64-byte record per child (AoS, one
+// scalar load each): c.xyz u.xyz v.xyz w.xyz h.xyz, then the child ref.  A child ref with kObbFlag set
+// names one of these nodes (index in Bvh::obb).
+constexpr uint32_t kObbFlag = 0x40000000u;
+struct Bvh4ObbChild {
+  float f[15];
+  uint32_t child;
+};
+struct Bvh4ObbNode {
+  Bvh4ObbChild c[4];
+};
+static_assert(sizeof(Bvh4ObbNode) == 256, "Bvh4ObbNode layout");
+
 struct Bvh {
   std::vector<Bvh4Node> nodes4;    // device BVH, root = 0 (always present)
+  std::vector<Bvh4ObbNode> obb;    // the wide subtree's nodes (refs kObbFlag | index)
+  std::vector<float> patch_obb;    // per patch (mesh order): c, u, v, w, h (15 floats) + 1 if it has one
   std::vector<BvhNode> nodes;      // binary build tree (one patch per leaf), root = 0
   std::vector<uint32_t> order;     // leaf ranges index this: patch index in mesh order
   std::vector<float> patch_box;    // per order slot: lo.xyz, 0, hi.xyz, 0 (the gate-region box)

@@ -14,9 +14,14 @@ int32_t bzr_debug_gate_boxes(const void *patches, uint32_t n, uint32_t stride, f
  * origins |s|_inf <= *s_max, which is 8x the mesh's control-point span). */
 int32_t bzr_debug_gate_boxes_tier(const void *patches, uint32_t n, uint32_t stride, int32_t tier, float *boxes,
                                   float *s_max);
+/* The oriented gate-region boxes of one tier's wide-patch subtree (bvh.hpp Bvh4ObbNode), by patch index:
+ * out[16*i] = centre xyz, axes u v w (xyz each), half extents (3), then 1.0f if patch i is a wide patch
+ * (its parent node tests this box) or 0.0f (16 zeros: the patch is AABB-culled).  Returns 0 on success. */
+int32_t bzr_debug_gate_obbs(const void *patches, uint32_t n, uint32_t stride, int32_t tier, float *out);
 /* The bounding sphere bzr_illuminate culls with (Ritter over the gate boxes): centre xyz, radius. */
 int32_t bzr_debug_bounding_sphere(const void *patches, uint32_t n, uint32_t stride, float out[4]);
-/* Host replay of the device BVH walk (same 4-wide trees and wave-uniform tier choice, same float slab test) over `nr` rays in SoA
+/* Host replay of the device BVH walk (same 4-wide trees and wave-uniform tier choice, same float slab and
+ * oriented-box tests -- 1/x where the device uses v_rcp_f32) over `nr` rays in SoA
  * [6, nr], grouped in waves of 64 consecutive rays.  hits (optional, nr x n bytes): hits[r*n + b] = 1
  * when ray r reaches patch b's leaf box -- a superset of the patches whose planar gate it passes.
  * stats[0] node visits (per wave), [1] leaf records fetched (per wave), [2] leaf-box hits (per ray),

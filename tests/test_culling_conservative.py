@@ -149,3 +149,83 @@ def test_near_tier_is_tighter(bzr):
     ok = np.isfinite(far).all(axis=1) & (far[:, :3] <= far[:, 3:]).all(axis=1)
     assert (near[ok, :3] >= far[ok, :3]).all() and (near[ok, 3:] <= far[ok, 3:]).all()
     assert (near[ok, 3:] - near[ok, :3]).sum() < 0.99 * (far[ok, 3:] - far[ok, :3]).sum()
+
+
+# ------------------------------------------------------------------ oriented boxes (wide patches)
+def gate_obbs(bzr, patches, tier):
+    L = bzr.lib()
+    fn = L.bzr_debug_gate_obbs
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int32, ctypes.c_void_p]
+    fn.restype = ctypes.c_int32
+    p = np.ascontiguousarray(patches, np.float32)
+    out = np.zeros((len(p), 16), np.float32)
+    assert fn(p.ctypes.data, len(p), 264, tier, out.ctypes.data) == 0
+    return out
+
+
+def obb_f32(obbs, rays):
+    """float32 replica of the kernel's obb_hit (1/x for v_rcp_f32): hit[r, i]."""
+    f = np.float32
+    s = rays[:3].T.astype(f)[:, None, :]
+    d = rays[3:].T.astype(f)[:, None, :]
+    r = (s - obbs[None, :, 0:3]).astype(f)
+    tn = np.full(r.shape[:2], -np.finfo(f).max, f)
+    tf = np.full(r.shape[:2], np.finfo(f).max, f)
+    with np.errstate(all="ignore"):
+        for a in range(3):
+            u = obbs[None, :, 3 + 3 * a:6 + 3 * a]
+            o = (r * u).sum(-1).astype(f)
+            dd = (d * u).sum(-1).astype(f)
+            dd = np.where(np.abs(dd) < f(1e-20), np.copysign(f(1e-20), dd), dd).astype(f)
+            inv = (f(1) / dd).astype(f)
+            h = obbs[None, :, 12 + a]
+            t1, t2 = ((-h - o) * inv).astype(f), ((h - o) * inv).astype(f)
+            tn, tf = np.fmax(tn, np.fmin(t1, t2)), np.fmin(tf, np.fmax(t1, t2))
+    return (tn <= tf) & (tf >= 0)
+
+
+def ill_conditioned(patches):
+    """kappa = gamma_3 l1 sum|q| >= 1/2 (bvh.cpp): the patches whose float gate is rounding-dominated."""
+    M = patches[:, 49:58].astype(np.float64).reshape(-1, 3, 3).transpose(0, 2, 1)
+    fin = np.isfinite(M).all(axis=(1, 2))
+    Mf = np.where(fin[:, None, None], M, np.eye(3))
+    l1 = np.abs(Mf).sum(axis=2).max(axis=1)
+    q = np.abs(np.linalg.inv(Mf)).max(axis=1).sum(axis=1)
+    return np.nonzero(fin & (3.0000002 * 2.0 ** -24 * l1 * q >= 0.5))[0]
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("tier", TIERS)
+def test_ill_conditioned_patches_never_culled(bzr, orc, tier):
+    """cfg5's ~1200 rounding-dominated patches (planes through ~the origin): every gate pass
+    of config rays and of rays aimed at those patches from near the origin must hit both the patch's AABB and,
+    for wide patches, its oriented box.  (Before the untruncated region clip, hundreds were missed.)"""
+    cfg = CONFIGS["cfg5"]
+    patches = build_lens(bzr.TriMesh, cfg.lenses[0]).bezier_patches()
+    ill = ill_conditioned(patches)
+    assert len(ill) > 1000
+    boxes, smax = gate_boxes(bzr, patches, tier)
+    obbs = gate_obbs(bzr, patches, tier)[ill]
+    pi, bi = patches[ill], boxes[ill]
+    rng = np.random.default_rng(17 + tier)
+    from bzr_amd.configs import pixel_coords, rays_for
+    r, c = pixel_coords(cfg, side=8192, order="rows")
+    pick = rng.choice(len(r), 20000, replace=False)
+    n = 20000
+    o = rng.uniform(-6, 6, (n, 3))
+    o[:, 0] = rng.uniform(-2, 2, n)
+    tgt = pi[rng.integers(0, len(ill), n), 19:22] + rng.normal(size=(n, 3)) * 0.5
+    d = tgt - o
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    passes = 0
+    for rays in (rays_for(cfg, r[pick], c[pick], side=8192), np.concatenate([o.T, d.T]).astype(np.float32)):
+        near = np.abs(rays[:3]).max(axis=0) <= smax
+        gate = orc.planar_gate(pi, rays, threads=8) & near[:, None]
+        ri, pj = np.nonzero(gate)
+        passes += len(ri)
+        ur = np.unique(ri)
+        k = np.searchsorted(ur, ri)
+        assert slab_f32(bi, rays[:, ur])[k, pj].all()
+        wide = obbs[:, 15] > 0
+        assert (obb_f32(obbs, rays[:, ur])[k, pj] | ~wide[pj]).all()
+    assert passes > 200

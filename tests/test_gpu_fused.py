@@ -60,15 +60,15 @@ def test_intersect_and_refract_fused_equal_staged(bzr, ctx, cfg2_lens):
     assert (fs != 0).any()
 
 
-def test_fast_mode_fused_equals_staged(bzr, ctx, cfg2_lens):
-    """FAST runs the same fast:: Newton arithmetic in both pipelines (the exact gate recomputed in k_trace
-    gives the same (cos, t) as the staged path's skipped gate), so they agree bit for bit too."""
+def test_fast_mode_fused_agrees_with_staged(bzr, ctx, cfg2_lens):
+    """FAST (not bit-exact by design) in the two pipelines: both see the reference's candidates (exact
+    gate); their fast:: Newton code is compiled separately, so FMA contraction may differ.  They must
+    agree within SURVEY 8c's fast-mode gates: status >= 99.5 %, segment counts >= 99 %."""
     rays = grid_rays(CONFIGS["cfg2"], side=192)
     dm = bzr.DeviceMesh(ctx, cfg2_lens)
-    f = bzr.trace_chain(ctx, [dm], [1.3], rays, mode=bzr.MODE_FAST | bzr.PIPELINE_FUSED)
-    s = bzr.trace_chain(ctx, [dm], [1.3], rays, mode=bzr.MODE_FAST | bzr.PIPELINE_STAGED)
-    for a, b in zip(f, s):
-        assert np.array_equal(u32(a), u32(b))
+    fo, fs, fg = bzr.trace_chain(ctx, [dm], [1.3], rays, mode=bzr.MODE_FAST | bzr.PIPELINE_FUSED)
+    so, ss, sg = bzr.trace_chain(ctx, [dm], [1.3], rays, mode=bzr.MODE_FAST | bzr.PIPELINE_STAGED)
+    assert (fs == ss).mean() >= 0.995 and (fg == sg).mean() >= 0.99
 
 
 def test_far_origins_take_the_inline_full_scan(bzr, orc, ctx):

@@ -331,3 +331,31 @@ def test_culled_equals_bruteforce_cfg3_full(bzr, ctx, meshes, pipe):
     b = bzr.intersect(ctx, dm, rays, mode=bzr.ACCEL_NONE)
     assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
     assert abs((a.view(np.uint32)[11] == 4).mean() - 0.2505) < 0.001  # 25.05 % of the 2048^2 grid (27.0 % on a 64^2 grid)
+
+
+@pytest.mark.slow
+def test_culled_equals_bruteforce_cfg5_ill_conditioned(bzr, ctx, pipe):
+    """cfg5 (301 056 patches, ~1200 of them rounding-dominated): culled == brute force on
+    131 072 grid rays and 131 072 rays from near the origin aimed at the ill-conditioned patches."""
+    cfg = CONFIGS["cfg5"]
+    patches = build_lens(bzr.TriMesh, cfg.lenses[0]).bezier_patches()
+    M = patches[:, 49:58].astype(np.float64).reshape(-1, 3, 3).transpose(0, 2, 1)
+    fin = np.isfinite(M).all(axis=(1, 2))
+    Mf = np.where(fin[:, None, None], M, np.eye(3))
+    kappa = 3.0000002 * 2.0 ** -24 * np.abs(Mf).sum(axis=2).max(axis=1) * np.abs(np.linalg.inv(Mf)).max(axis=1).sum(axis=1)
+    ill = np.nonzero(fin & (kappa >= 0.5))[0]
+    rng = np.random.default_rng(55)
+    r, c = pixel_coords(cfg, side=8192, order="tiles")
+    start = rng.integers(0, len(r) // 64 - 2048) * 64
+    grid = rays_for(cfg, r[start:start + 131072], c[start:start + 131072], side=8192)
+    n = 131072
+    o = rng.uniform(-6, 6, (n, 3))
+    o[:, 0] = rng.uniform(-2, 2, n)
+    tgt = patches[ill[rng.integers(0, len(ill), n)], 19:22] + rng.normal(size=(n, 3)) * 0.5
+    d = (tgt - o) / np.linalg.norm(tgt - o, axis=1, keepdims=True)
+    rays = np.concatenate([grid, np.concatenate([o.T, d.T]).astype(np.float32)], axis=1)
+    dm = bzr.DeviceMesh(ctx, patches)
+    a = bzr.intersect(ctx, dm, rays, mode=pipe)
+    b = bzr.intersect(ctx, dm, rays, mode=bzr.ACCEL_NONE)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    assert (a.view(np.uint32)[11] == 4).mean() > 0.2
