@@ -877,9 +877,29 @@ constexpr int kHitWords = 12;  // t, point, cos, bary, normal, source patch
 #ifndef BZR_TRACE_LDS_RECORD
 #define BZR_TRACE_LDS_RECORD 0
 #endif
+// BZR_TRACE_DEFER (A/B knob): the wave first collects the leaves of its walk whose gate passed (up to
+// kEntries) and then runs their Newton passes in order; a follow-side retry whose neighbour is one of the
+// collected leaves still to come joins that leaf's pass (its lanes keep their own scan index and limit)
+// instead of taking a pass of its own.
+#ifndef BZR_TRACE_DEFER
+#define BZR_TRACE_DEFER 1
+#endif
+#ifndef BZR_TRACE_ENTRIES
+#define BZR_TRACE_ENTRIES 16
+#endif
+// BZR_TRACE_LIFO (A/B knob): run the collected leaves last-found first
+#ifndef BZR_TRACE_LIFO
+#define BZR_TRACE_LIFO 0
+#endif
+constexpr uint32_t kEntries = BZR_TRACE_ENTRIES;  // power of two, <= 64
+static_assert(kEntries >= 4 && kEntries <= 64 && (kEntries & (kEntries - 1)) == 0, "kEntries");
 struct TraceLds {              // per wave
   uint32_t stack[kStack];
   float hit[kHitWords][64];    // the lane's current winner (written only when it improves)
+#if BZR_TRACE_DEFER
+  unsigned long long emask[kEntries];  // collected leaves: gate ballot
+  uint32_t eid[kEntries];              // and patch index
+#endif
 #if BZR_TRACE_LDS_RECORD
   float rec[2][rec::kWords];
 #endif
@@ -1027,6 +1047,148 @@ __device__ __forceinline__ void trace_segment(const MeshView &m, f3 s, f3 d, boo
   }
 }
 
+#if BZR_TRACE_DEFER
+__device__ __forceinline__ unsigned long long uniform_u64(unsigned long long v) {
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)), lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  return ((unsigned long long)hi << 32) | lo;  // (readfirstlane returns int: widen the unsigned halves)
+}
+__device__ __forceinline__ bool lane_bit(unsigned long long m, uint32_t lane) { return ((m >> lane) & 1ull) != 0ull; }
+
+// trace_segment with the collected-leaves schedule (BZR_TRACE_DEFER): same candidates, same Newton calls
+// per (lane, patch, limit), same (t order, scan index) keys -- only the passes are grouped differently.
+template <bool kFast, bool kCount>
+__device__ __forceinline__ void trace_segment_defer(const MeshView &m, f3 s, f3 d, bool act, unsigned long long &best,
+                                                    TraceLds &L, uint32_t lane, TraceCtr &ctr) {
+  best = ~0ull;
+  const float amax = fmaxf(fmaxf(fabsf(s.x), fabsf(s.y)), fabsf(s.z));
+  bool ovf = false;  // this lane takes the in-order full scan
+  if (act && !(amax <= m.s_max)) {
+    ovf = true;
+    act = false;
+  }
+  const bool near_tier = !__any(act && !(amax <= m.s_near));
+  const bzr_host::Bvh4Node *nodes = near_tier ? m.nodes_near : m.nodes;
+  const bzr_host::Bvh4ObbNode *obb = near_tier ? m.obb_near : m.obb;
+  const float4 *leaf = near_tier ? m.leaf_near : m.leaf;
+  const f3 inv = mk(safe_inv(d.x), safe_inv(d.y), safe_inv(d.z));
+  const f3 sinv = mk(s.x * inv.x, s.y * inv.y, s.z * inv.z);
+  int sp = 0;
+  if (m.n > 0 && __any(act)) {
+    L.stack[0] = 0u;
+    sp = 1;
+  }
+  uint32_t scan = 0xFFFFFFFFu;  // next patch of the full scan (0xFFFFFFFF: not scanning)
+  uint32_t fnb = 0xFFFFFFFFu, fsrc = 0u;  // this lane's deferred follow-side retry: neighbour, scanned patch
+  for (;;) {
+    uint32_t ne = 0;  // collected leaves (uniform)
+    while (sp > 0 && ne + 4u <= kEntries) {
+      const uint32_t node = __builtin_amdgcn_readfirstlane(L.stack[--sp]);
+      if (kCount) ++ctr.nodes;
+      bool hit[4];
+      uint32_t ch[4];
+      node_children(nodes, obb, node, act, s, d, sinv, inv, hit, ch);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const unsigned long long hm = __ballot(hit[c]);
+        if (hm == 0ull) continue;
+        if (ch[c] & bzr_host::kLeafFlag) {
+          const u32x16 r = *((const cu32x16 *)(uintptr_t)leaf + (ch[c] & ~bzr_host::kLeafFlag));
+          const float4 g0 = make_float4(__uint_as_float(r[0]), __uint_as_float(r[1]), __uint_as_float(r[2]), __uint_as_float(r[3]));
+          const float4 g1 = make_float4(__uint_as_float(r[4]), __uint_as_float(r[5]), __uint_as_float(r[6]), __uint_as_float(r[7]));
+          const float4 g2 = make_float4(__uint_as_float(r[8]), __uint_as_float(r[9]), __uint_as_float(r[10]), __uint_as_float(r[11]));
+          const float4 g3 = make_float4(__uint_as_float(r[12]), __uint_as_float(r[13]), __uint_as_float(r[14]), 0.0f);
+          const bool pass = hit[c] && planar_gate(g0, g1, g2, g3, s, d);
+          if (kCount) {
+            ++ctr.leaves;
+            ctr.gate_tests += popc64(hm);
+          }
+          const unsigned long long pm = __ballot(pass);
+          if (pm) {
+            if (lane == 0u) {
+              L.eid[ne] = r[15];
+              L.emask[ne] = pm;
+            }
+            ++ne;
+          }
+        } else if (sp < kStack) {
+          L.stack[sp++] = ch[c];
+        } else {  // traversal stack exhausted: these lanes take the full scan
+          if (hit[c]) ovf = true;
+        }
+      }
+    }
+    if (ne == 0u) {  // tree done: the reference's in-order scan for the lanes that could not use it
+      if (scan == 0xFFFFFFFFu) {
+        if (!__any(ovf)) break;
+        scan = 0;
+        if (kCount) ctr.ovf += popc64(__ballot(ovf));
+      }
+      bool pass = false;
+      for (; scan < m.n; ++scan) {
+        const float4 *g = m.planar + 4u * scan;  // wave-uniform address -> scalar loads
+        pass = ovf && planar_gate(g[0], g[1], g[2], g[3], s, d);
+        if (__any(pass)) break;
+      }
+      if (scan >= m.n) break;
+      const unsigned long long pm = __ballot(pass);
+      if (lane == 0u) {
+        L.eid[0] = scan;
+        L.emask[0] = pm;
+      }
+      ne = 1;
+      ++scan;
+    }
+    // Newton passes over the collected leaves, in order
+    for (uint32_t k = 0; k < ne; ++k) {
+      const uint32_t e = BZR_TRACE_LIFO ? ne - 1u - k : k;
+      const uint32_t b = __builtin_amdgcn_readfirstlane(L.eid[e]);
+      const bool run0 = lane_bit(uniform_u64(L.emask[e]), lane);
+      const bool joined = fnb == b;  // an earlier leaf's follow-side retry on this one
+      const uint32_t sidx = joined ? fsrc : b;
+      if (joined) fnb = 0xFFFFFFFFu;
+      if (kCount) {
+        ++ctr.rounds;
+        ctr.pairs += popc64(__ballot(run0));
+        ctr.follows += popc64(__ballot(joined));
+      }
+      const auto hp = uniform_patch(m.full, b);
+      uint32_t what = kNone;
+      if (run0 || joined) {
+        const Hit h = patch_intersect<false, kFast>(hp, s, d, joined);
+        consider(h, sidx, b, best, L, lane);
+        if (!joined) what = h.what;
+      }
+      for (uint32_t side = 0; side < 3u; ++side) {
+        bool fl = run0 && what == side;
+        if (!__any(fl)) continue;
+        const uint32_t nb = __float_as_uint(hp.r[rec::kNeigh + side]);
+        // the neighbour among the leaves still to come: defer the retry into its pass
+        const bool to_come = BZR_TRACE_LIFO ? lane < e : (lane > e && lane < ne);
+        const unsigned long long later = __ballot(to_come && L.eid[lane & (kEntries - 1u)] == nb);
+        if (later) {
+          const unsigned long long fm = uniform_u64(L.emask[__builtin_ctzll(later)]);
+          if (fl && fnb == 0xFFFFFFFFu && !lane_bit(fm, lane)) {
+            fnb = nb;
+            fsrc = b;
+            fl = false;
+          }
+        }
+        if (!__any(fl)) continue;
+        if (kCount) {
+          ++ctr.rounds;
+          ctr.follows += popc64(__ballot(fl));
+        }
+        const auto pa = uniform_patch(m.full, nb);
+        if (fl) {
+          const Hit h = patch_intersect<false, kFast>(pa, s, d, true);
+          consider(h, b, nb, best, L, lane);
+        }
+      }
+    }
+  }
+}
+#endif
+
 // Trace job of one launch.  Modes: kModeHits (one BezierMesh::intersect per ray -> hits), kModeRefract
 // (one BezierLens::refract -> ray', status), kModeStage (the chain over lenses [0, count): refract(INSIDE)
 // then refract(OUTSIDE) per lens, a NONE ends the ray -- reference/test.cpp:376-401).
@@ -1072,7 +1234,11 @@ __global__ __launch_bounds__(kBlock) BZR_TRACE_ATTR void k_trace(LensSet lenses,
     if (!__any(alive)) break;
     const MeshView &m = lenses.lens[k >> 1];
     unsigned long long best;
+#if BZR_TRACE_DEFER
+    trace_segment_defer<kFast, kCount>(m, s, d, alive, best, L, lane, ctr);
+#else
     trace_segment<kFast, kCount>(m, s, d, alive, best, L, lane, ctr);
+#endif
     if (kCount) ctr.segments += popc64(__ballot(alive));
     Hit h = no_hit();
     uint32_t patch = 0xFFFFFFFFu;
