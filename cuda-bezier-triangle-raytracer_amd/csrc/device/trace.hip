@@ -853,11 +853,13 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_small(uint32_t *__restric
 // ------------------------------------------------------------ fused path (default)
 // One kernel per call: each wave takes 64 rays and runs every segment of them (one BezierMesh::intersect,
 // or the whole refraction chain) without leaving the wave.  The wave walks the lens BVH as k_traverse
-// does; each leaf whose exact planar gate passes for some lanes is queued (wave-uniform patch index +
-// lane mask, at most the 4 children of one node), and the queue is drained through ONE Newton site:
-// the lanes that passed run BezierTriangle::intersect with the patch record in SGPRs (uniform
-// constant-address loads), then, side by side, the follow-side retries on the named neighbours
-// (reference/bezierMesh.cpp:212-216; the neighbour of side K is uniform too).  Each lane keeps the
+// does; each leaf whose exact planar gate passes for some lanes is collected (wave-uniform patch index +
+// lane mask, in LDS: trace_segment_defer; trace_segment is the older schedule that drains a 4-entry queue
+// after every node), and the collected leaves run through ONE Newton site: the lanes that passed run
+// BezierTriangle::intersect with the patch record in SGPRs (uniform constant-address loads), then the
+// follow-side retries on the named neighbours (reference/bezierMesh.cpp:212-216; the neighbour of side
+// K is uniform too), which join the neighbour's own pass when it is a collected leaf still to come.
+// Each lane keeps the
 // lexicographic minimum of (t order key, scanned patch index) -- the reference's strict-< in-order
 // winner, as in the staged path -- with the winning hit in LDS.  Nothing per pair leaves the CU: HBM
 // sees the rays in and the results out.  A patch sits in one leaf, so a wave runs Newton at most once
