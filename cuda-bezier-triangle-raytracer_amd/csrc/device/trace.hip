@@ -852,20 +852,25 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_small(uint32_t *__restric
 
 // ------------------------------------------------------------ fused path (default)
 // One kernel per call: each wave takes 64 rays and runs every segment of them (one BezierMesh::intersect,
-// or the whole refraction chain) without leaving the wave.  The wave walks the lens BVH as k_traverse
-// does; each leaf whose exact planar gate passes for some lanes is collected (wave-uniform patch index +
-// lane mask, in LDS: trace_segment_defer; trace_segment is the older schedule that drains a 4-entry queue
-// after every node), and the collected leaves run through ONE Newton site: the lanes that passed run
-// BezierTriangle::intersect with the patch record in SGPRs (uniform constant-address loads), then the
-// follow-side retries on the named neighbours (reference/bezierMesh.cpp:212-216; the neighbour of side
-// K is uniform too), which join the neighbour's own pass when it is a collected leaf still to come.
-// Each lane keeps the
-// lexicographic minimum of (t order key, scanned patch index) -- the reference's strict-< in-order
-// winner, as in the staged path -- with the winning hit in LDS.  Nothing per pair leaves the CU: HBM
-// sees the rays in and the results out.  A patch sits in one leaf, so a wave runs Newton at most once
-// per (patch, segment); the lanes that do not need it idle through that pass (lane utilisation is the
-// wave's pairs / (64 x distinct patches)).  Rays whose origin lies beyond the tree's
-// validity radius, or whose stack overflows, take the reference's in-order scan in the same wave
+// or the whole refraction chain) without leaving the wave.  Per segment (trace_segment):
+//  - the wave walks the lens BVH as k_traverse does and collects, in LDS, each leaf whose exact planar
+//    gate passes for some lanes (wave-uniform patch index + lane mask, up to kEntries per batch);
+//  - the collected leaves run through ONE Newton site, in order: the lanes that passed run
+//    BezierTriangle::intersect with the patch record in SGPRs (uniform constant-address loads); lanes
+//    whose result is follow-side K retry the named neighbour with cNone (reference/bezierMesh.cpp:212-216;
+//    the neighbour of side K is uniform too).  A retry whose neighbour is a collected leaf still to come
+//    joins that leaf's pass; one whose neighbour already ran takes the result that pass parked for it
+//    (below); only the rest take a pass of their own;
+//  - parking (BZR_TRACE_SPEC): a leaf's pass also runs, in its otherwise idle lanes, the cNone evaluation
+//    for the lanes of later leaves that neighbour it -- the retry those lanes would ask for -- and parks
+//    the result in LDS (one per lane and segment; not for kModeHits, whose 12-word winner leaves no room).
+// Each lane keeps the lexicographic minimum of (t order key, scanned patch index) -- the reference's
+// strict-< in-order winner, as in the staged path -- with the winning hit in LDS.  The schedule decides
+// which pass evaluates a (lane, patch, limit), never the evaluation or its key.  Nothing per pair leaves
+// the CU: HBM sees the rays in and the results out.  A patch sits in one leaf, so a wave runs a patch's
+// pass at most once per segment (plus retries that could neither join nor use a parked result); lanes
+// that need neither idle through it (lane utilisation).  Rays whose origin lies beyond the
+// tree's validity radius, or whose stack overflows, take the reference's in-order scan in the same wave
 // (same Newton site, patches in index order).
 // Device work counters (bzr_ctx_counters) are kept in this many copies, summed by the report: a wave adds
 // to copy (wave index mod kCounterReplicas), so a frame's ~10^5 waves do not queue on 8 addresses.
@@ -873,194 +878,126 @@ constexpr uint32_t kCounterReplicas = 64;
 struct TraceCtr {  // wave-uniform work counters (kCount)
   uint32_t nodes = 0, leaves = 0, gate_tests = 0, rounds = 0, pairs = 0, follows = 0, segments = 0, ovf = 0;
 };
-constexpr int kHitWords = 12;  // t, point, cos, bary, normal, source patch
-// BZR_TRACE_LDS_RECORD (A/B knob, default 0): the Newton site reads the patch record from a per-wave LDS
-// copy (volatile per-use ds_reads) instead of SGPRs -- the operand path a per-lane-record pass would use.
-#ifndef BZR_TRACE_LDS_RECORD
-#define BZR_TRACE_LDS_RECORD 0
-#endif
-// BZR_TRACE_DEFER (A/B knob): the wave first collects the leaves of its walk whose gate passed (up to
-// kEntries) and then runs their Newton passes in order; a follow-side retry whose neighbour is one of the
-// collected leaves still to come joins that leaf's pass (its lanes keep their own scan index and limit)
-// instead of taking a pass of its own.
-#ifndef BZR_TRACE_DEFER
-#define BZR_TRACE_DEFER 1
-#endif
 #ifndef BZR_TRACE_ENTRIES
 #define BZR_TRACE_ENTRIES 16
 #endif
-// BZR_TRACE_LIFO (A/B knob): run the collected leaves last-found first
-#ifndef BZR_TRACE_LIFO
-#define BZR_TRACE_LIFO 0
+#ifndef BZR_TRACE_SPEC
+#define BZR_TRACE_SPEC 1
 #endif
-constexpr uint32_t kEntries = BZR_TRACE_ENTRIES;  // power of two, <= 64
+constexpr uint32_t kEntries = BZR_TRACE_ENTRIES;  // collected leaves per batch: power of two, <= 64
 static_assert(kEntries >= 4 && kEntries <= 64 && (kEntries & (kEntries - 1)) == 0, "kEntries");
-struct TraceLds {              // per wave
-  uint32_t stack[kStack];
-  float hit[kHitWords][64];    // the lane's current winner (written only when it improves)
-#if BZR_TRACE_DEFER
-  unsigned long long emask[kEntries];  // collected leaves: gate ballot
-  uint32_t eid[kEntries];              // and patch index
-#endif
-#if BZR_TRACE_LDS_RECORD
-  float rec[2][rec::kWords];
-#endif
+// Words kept per lane: the winner (all of BezierIntersection for kModeHits; what refraction reads
+// otherwise: point, cos, normal) and a parked retry result (t, point, cos, normal).
+template <int kMode>
+struct TraceWords {
+  static constexpr int kHit = kMode == kModeHits ? 12 : 7;
+  static constexpr int kPark = (kMode != kModeHits && BZR_TRACE_SPEC) ? 8 : 0;
 };
-typedef __attribute__((address_space(3))) const volatile float lds_vfloat;
+template <int kMode>
+struct TraceLds {  // per wave
+  uint32_t stack[kStack];
+  float hit[TraceWords<kMode>::kHit][64];    // the lane's current winner (written only when it improves)
+  unsigned long long emask[kEntries];        // collected leaves: gate ballot
+  uint32_t eid[kEntries];                    // and patch index
+  float park[TraceWords<kMode>::kPark ? TraceWords<kMode>::kPark : 1][64];
+};
 
 __device__ __forceinline__ uint32_t popc64(unsigned long long m) { return (uint32_t)__popcll(m); }
-
-// The lane's candidate `h` from scanned patch `scan` (the hit itself from patch `src`).
-__device__ __forceinline__ void consider(const Hit &h, uint32_t scan, uint32_t src, unsigned long long &best,
-                                         TraceLds &L, uint32_t lane) {
-  if (h.what == kIntersect && h.t < FLT_MAX) {
-    const unsigned long long k = ((unsigned long long)t_order(h.t) << 32) | scan;
-    if (k < best) {
-      best = k;
-      L.hit[0][lane] = h.t;
-      L.hit[1][lane] = h.point.x;
-      L.hit[2][lane] = h.point.y;
-      L.hit[3][lane] = h.point.z;
-      L.hit[4][lane] = h.cs;
-      L.hit[5][lane] = h.bary.x;
-      L.hit[6][lane] = h.bary.y;
-      L.hit[7][lane] = h.bary.z;
-      L.hit[8][lane] = h.normal.x;
-      L.hit[9][lane] = h.normal.y;
-      L.hit[10][lane] = h.normal.z;
-      L.hit[11][lane] = __uint_as_float(src);
-    }
-  }
-}
-
-// One BezierMesh::intersect for the wave's active lanes; the winner is left in `best` / L.hit.
-template <bool kFast, bool kCount>
-__device__ __forceinline__ void trace_segment(const MeshView &m, f3 s, f3 d, bool act, unsigned long long &best,
-                                              TraceLds &L, uint32_t lane, TraceCtr &ctr) {
-  best = ~0ull;
-  const float amax = fmaxf(fmaxf(fabsf(s.x), fabsf(s.y)), fabsf(s.z));
-  bool ovf = false;  // this lane takes the in-order full scan
-  if (act && !(amax <= m.s_max)) {
-    ovf = true;
-    act = false;
-  }
-  const bool near_tier = !__any(act && !(amax <= m.s_near));
-  const bzr_host::Bvh4Node *nodes = near_tier ? m.nodes_near : m.nodes;
-  const bzr_host::Bvh4ObbNode *obb = near_tier ? m.obb_near : m.obb;
-  const float4 *leaf = near_tier ? m.leaf_near : m.leaf;
-  const f3 inv = mk(safe_inv(d.x), safe_inv(d.y), safe_inv(d.z));
-  const f3 sinv = mk(s.x * inv.x, s.y * inv.y, s.z * inv.z);
-  int sp = 0;
-  if (m.n > 0 && __any(act)) {
-    L.stack[0] = 0u;
-    sp = 1;
-  }
-  // leaf queue: wave-uniform patch indices + per-lane gate results (LIFO, fixed slots)
-  uint32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0, qn = 0;
-  bool p0 = false, p1 = false, p2 = false, p3 = false;
-  uint32_t scan = 0xFFFFFFFFu;  // next patch of the full scan (0xFFFFFFFF: not scanning)
-  for (;;) {
-    if (qn == 0) {
-      if (sp > 0) {
-        const uint32_t node = __builtin_amdgcn_readfirstlane(L.stack[--sp]);
-        if (kCount) ++ctr.nodes;
-        bool hit[4];
-        uint32_t ch[4];
-        node_children(nodes, obb, node, act, s, d, sinv, inv, hit, ch);
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const unsigned long long hm = __ballot(hit[c]);
-          if (hm == 0ull) continue;
-          if (ch[c] & bzr_host::kLeafFlag) {
-            const u32x16 r = *((const cu32x16 *)(uintptr_t)leaf + (ch[c] & ~bzr_host::kLeafFlag));
-            const float4 g0 = make_float4(__uint_as_float(r[0]), __uint_as_float(r[1]), __uint_as_float(r[2]), __uint_as_float(r[3]));
-            const float4 g1 = make_float4(__uint_as_float(r[4]), __uint_as_float(r[5]), __uint_as_float(r[6]), __uint_as_float(r[7]));
-            const float4 g2 = make_float4(__uint_as_float(r[8]), __uint_as_float(r[9]), __uint_as_float(r[10]), __uint_as_float(r[11]));
-            const float4 g3 = make_float4(__uint_as_float(r[12]), __uint_as_float(r[13]), __uint_as_float(r[14]), 0.0f);
-            const bool pass = hit[c] && planar_gate(g0, g1, g2, g3, s, d);
-            if (kCount) {
-              ++ctr.leaves;
-              ctr.gate_tests += popc64(hm);
-            }
-            if (__any(pass)) {
-              q3 = q2; q2 = q1; q1 = q0; q0 = r[15];
-              p3 = p2; p2 = p1; p1 = p0; p0 = pass;
-              ++qn;
-            }
-          } else if (sp < kStack) {
-            L.stack[sp++] = ch[c];
-          } else {  // traversal stack exhausted: these lanes take the full scan
-            if (hit[c]) ovf = true;
-          }
-        }
-        continue;
-      }
-      // tree done: the reference's in-order scan for the lanes that could not use it
-      if (scan == 0xFFFFFFFFu) {
-        if (!__any(ovf)) break;
-        scan = 0;
-        if (kCount) ctr.ovf += popc64(__ballot(ovf));
-      }
-      bool pass = false;
-      for (; scan < m.n; ++scan) {
-        const float4 *g = m.planar + 4u * scan;  // wave-uniform address -> scalar loads
-        pass = ovf && planar_gate(g[0], g[1], g[2], g[3], s, d);
-        if (__any(pass)) break;
-      }
-      if (scan >= m.n) break;
-      q0 = scan++;
-      p0 = pass;
-      qn = 1;
-    }
-    // Newton site: the queue head's patch for the lanes that passed its gate, then its follow-side
-    // neighbours (limit cNone) for the lanes that asked for them; all ordered by the head's index.
-    const uint32_t b = q0;
-    const bool run0 = p0;
-    q0 = q1; q1 = q2; q2 = q3;
-    p0 = p1; p1 = p2; p2 = p3;
-    --qn;
-    const auto hp = uniform_patch(m.full, b);
-    uint32_t pb = b, side = 0, what = kNone;
-    bool lim = false, run = run0;
-    for (;;) {
-      if (kCount) {
-        ++ctr.rounds;
-        if (lim) ctr.follows += popc64(__ballot(run));
-        else ctr.pairs += popc64(__ballot(run));
-      }
-#if BZR_TRACE_LDS_RECORD
-      for (uint32_t k = lane; k < (uint32_t)rec::kWords; k += 64u) L.rec[0][k] = m.full[(size_t)rec::kWords * pb + k];
-      const PatchView<lds_vfloat *> pa{(lds_vfloat *)&L.rec[0][0]};
-#else
-      const auto pa = uniform_patch(m.full, pb);
-#endif
-      if (run) {
-        const Hit h = patch_intersect<false, kFast>(pa, s, d, lim);
-        consider(h, b, pb, best, L, lane);
-        if (!lim) what = h.what;
-      }
-      while (side < 3u && !__any(run0 && what == side)) ++side;
-      if (side >= 3u) break;
-      pb = __float_as_uint(hp.r[rec::kNeigh + side]);
-      run = run0 && what == side;
-      lim = true;
-      ++side;
-    }
-  }
-}
-
-#if BZR_TRACE_DEFER
 __device__ __forceinline__ unsigned long long uniform_u64(unsigned long long v) {
   const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)), lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
   return ((unsigned long long)hi << 32) | lo;  // (readfirstlane returns int: widen the unsigned halves)
 }
 __device__ __forceinline__ bool lane_bit(unsigned long long m, uint32_t lane) { return ((m >> lane) & 1ull) != 0ull; }
 
-// trace_segment with the collected-leaves schedule (BZR_TRACE_DEFER): same candidates, same Newton calls
-// per (lane, patch, limit), same (t order, scan index) keys -- only the passes are grouped differently.
-template <bool kFast, bool kCount>
-__device__ __forceinline__ void trace_segment_defer(const MeshView &m, f3 s, f3 d, bool act, unsigned long long &best,
-                                                    TraceLds &L, uint32_t lane, TraceCtr &ctr) {
+// The lane's candidate `h` from scanned patch `scan` (the hit itself from patch `src`).
+template <int kMode>
+__device__ __forceinline__ void consider(const Hit &h, uint32_t scan, uint32_t src, unsigned long long &best,
+                                         TraceLds<kMode> &L, uint32_t lane) {
+  if (h.what == kIntersect && h.t < FLT_MAX) {
+    const unsigned long long k = ((unsigned long long)t_order(h.t) << 32) | scan;
+    if (k < best) {
+      best = k;
+      if constexpr (kMode == kModeHits) {
+        L.hit[0][lane] = h.t;
+        L.hit[1][lane] = h.point.x;
+        L.hit[2][lane] = h.point.y;
+        L.hit[3][lane] = h.point.z;
+        L.hit[4][lane] = h.cs;
+        L.hit[5][lane] = h.bary.x;
+        L.hit[6][lane] = h.bary.y;
+        L.hit[7][lane] = h.bary.z;
+        L.hit[8][lane] = h.normal.x;
+        L.hit[9][lane] = h.normal.y;
+        L.hit[10][lane] = h.normal.z;
+        L.hit[11][lane] = __uint_as_float(src);
+      } else {
+        L.hit[0][lane] = h.point.x;
+        L.hit[1][lane] = h.point.y;
+        L.hit[2][lane] = h.point.z;
+        L.hit[3][lane] = h.cs;
+        L.hit[4][lane] = h.normal.x;
+        L.hit[5][lane] = h.normal.y;
+        L.hit[6][lane] = h.normal.z;
+      }
+    }
+  }
+}
+
+// The lane's winner back from LDS (best != ~0).
+template <int kMode>
+__device__ __forceinline__ Hit winner(TraceLds<kMode> &L, uint32_t lane, uint32_t &patch) {
+  Hit h = no_hit();
+  h.what = kIntersect;
+  if constexpr (kMode == kModeHits) {
+    h.t = L.hit[0][lane];
+    h.point = mk(L.hit[1][lane], L.hit[2][lane], L.hit[3][lane]);
+    h.cs = L.hit[4][lane];
+    h.bary = mk(L.hit[5][lane], L.hit[6][lane], L.hit[7][lane]);
+    h.normal = mk(L.hit[8][lane], L.hit[9][lane], L.hit[10][lane]);
+    patch = __float_as_uint(L.hit[11][lane]);
+  } else {  // refract_hit reads point, cos and normal
+    h.point = mk(L.hit[0][lane], L.hit[1][lane], L.hit[2][lane]);
+    h.cs = L.hit[3][lane];
+    h.normal = mk(L.hit[4][lane], L.hit[5][lane], L.hit[6][lane]);
+    patch = 0xFFFFFFFFu;
+  }
+  return h;
+}
+
+// A parked cNone result: t (NaN when it is not an intersection, which consider() drops like a miss),
+// point, cos, normal -- what consider() and the refraction read.
+template <int kMode>
+__device__ __forceinline__ void park(const Hit &h, TraceLds<kMode> &L, uint32_t lane) {
+  if constexpr (TraceWords<kMode>::kPark > 0) {
+    L.park[0][lane] = h.what == kIntersect ? h.t : __uint_as_float(0x7FC00000u);
+    L.park[1][lane] = h.point.x;
+    L.park[2][lane] = h.point.y;
+    L.park[3][lane] = h.point.z;
+    L.park[4][lane] = h.cs;
+    L.park[5][lane] = h.normal.x;
+    L.park[6][lane] = h.normal.y;
+    L.park[7][lane] = h.normal.z;
+  }
+}
+template <int kMode>
+__device__ __forceinline__ Hit parked(TraceLds<kMode> &L, uint32_t lane) {
+  Hit h = no_hit();
+  if constexpr (TraceWords<kMode>::kPark > 0) {
+    h.t = L.park[0][lane];
+    h.point = mk(L.park[1][lane], L.park[2][lane], L.park[3][lane]);
+    h.cs = L.park[4][lane];
+    h.normal = mk(L.park[5][lane], L.park[6][lane], L.park[7][lane]);
+    h.what = kIntersect;
+  }
+  return h;
+}
+
+// One BezierMesh::intersect for the wave's active lanes; the winner is left in `best` / L.hit.
+template <int kMode, bool kFast, bool kCount>
+__device__ __forceinline__ void trace_segment(const MeshView &m, f3 s, f3 d, bool act, unsigned long long &best,
+                                              TraceLds<kMode> &L, uint32_t lane, TraceCtr &ctr) {
+  constexpr bool kPark = TraceWords<kMode>::kPark > 0;
+  constexpr uint32_t kNo = 0xFFFFFFFFu;
   best = ~0ull;
   const float amax = fmaxf(fmaxf(fabsf(s.x), fabsf(s.y)), fabsf(s.z));
   bool ovf = false;  // this lane takes the in-order full scan
@@ -1079,8 +1016,9 @@ __device__ __forceinline__ void trace_segment_defer(const MeshView &m, f3 s, f3 
     L.stack[0] = 0u;
     sp = 1;
   }
-  uint32_t scan = 0xFFFFFFFFu;  // next patch of the full scan (0xFFFFFFFF: not scanning)
-  uint32_t fnb = 0xFFFFFFFFu, fsrc = 0u;  // this lane's deferred follow-side retry: neighbour, scanned patch
+  uint32_t scan = kNo;                // next patch of the full scan (kNo: not scanning)
+  uint32_t join = kNo, join_src = 0;  // a retry waiting for a later leaf's pass: that leaf, scanned patch
+  uint32_t parked_nb = kNo;           // the patch whose cNone result is parked for this lane
   for (;;) {
     uint32_t ne = 0;  // collected leaves (uniform)
     while (sp > 0 && ne + 4u <= kEntries) {
@@ -1120,7 +1058,7 @@ __device__ __forceinline__ void trace_segment_defer(const MeshView &m, f3 s, f3 
       }
     }
     if (ne == 0u) {  // tree done: the reference's in-order scan for the lanes that could not use it
-      if (scan == 0xFFFFFFFFu) {
+      if (scan == kNo) {
         if (!__any(ovf)) break;
         scan = 0;
         if (kCount) ctr.ovf += popc64(__ballot(ovf));
@@ -1140,38 +1078,61 @@ __device__ __forceinline__ void trace_segment_defer(const MeshView &m, f3 s, f3 
       ne = 1;
       ++scan;
     }
-    // Newton passes over the collected leaves, in order
-    for (uint32_t k = 0; k < ne; ++k) {
-      const uint32_t e = BZR_TRACE_LIFO ? ne - 1u - k : k;
+    // the collected leaves' passes, in order
+    for (uint32_t e = 0; e < ne; ++e) {
       const uint32_t b = __builtin_amdgcn_readfirstlane(L.eid[e]);
+      const auto hp = uniform_patch(m.full, b);
       const bool run0 = lane_bit(uniform_u64(L.emask[e]), lane);
-      const bool joined = fnb == b;  // an earlier leaf's follow-side retry on this one
-      const uint32_t sidx = joined ? fsrc : b;
-      if (joined) fnb = 0xFFFFFFFFu;
+      const bool joined = join == b;  // an earlier leaf's retry on this one
+      const uint32_t sidx = joined ? join_src : b;
+      if (joined) join = kNo;
+      bool spec = false;  // park this leaf's cNone result for lanes of later leaves that neighbour it
+      if (kPark && e + 1u < ne) {
+        unsigned long long sm = 0ull;
+#pragma unroll
+        for (uint32_t side = 0; side < 3u; ++side) {
+          const uint32_t nb = __float_as_uint(hp.r[rec::kNeigh + side]);
+          const unsigned long long later = __ballot(lane > e && lane < ne && L.eid[lane & (kEntries - 1u)] == nb);
+          if (later) sm |= uniform_u64(L.emask[__builtin_ctzll(later)]);
+        }
+        spec = lane_bit(sm, lane) && !run0 && !joined && parked_nb == kNo;
+      }
       if (kCount) {
         ++ctr.rounds;
         ctr.pairs += popc64(__ballot(run0));
         ctr.follows += popc64(__ballot(joined));
       }
-      const auto hp = uniform_patch(m.full, b);
       uint32_t what = kNone;
-      if (run0 || joined) {
-        const Hit h = patch_intersect<false, kFast>(hp, s, d, joined);
-        consider(h, sidx, b, best, L, lane);
-        if (!joined) what = h.what;
+      if (run0 || joined || spec) {
+        const Hit h = patch_intersect<false, kFast>(hp, s, d, joined || spec);
+        if (spec) {
+          park(h, L, lane);
+          parked_nb = b;
+        } else {
+          consider(h, sidx, b, best, L, lane);
+          if (!joined) what = h.what;
+        }
       }
       for (uint32_t side = 0; side < 3u; ++side) {
         bool fl = run0 && what == side;
         if (!__any(fl)) continue;
         const uint32_t nb = __float_as_uint(hp.r[rec::kNeigh + side]);
-        // the neighbour among the leaves still to come: defer the retry into its pass
-        const bool to_come = BZR_TRACE_LIFO ? lane < e : (lane > e && lane < ne);
-        const unsigned long long later = __ballot(to_come && L.eid[lane & (kEntries - 1u)] == nb);
+        if (kPark) {  // computed by an earlier pass
+          const bool use = fl && parked_nb == nb;
+          if (use) {
+            consider(parked(L, lane), b, nb, best, L, lane);
+            fl = false;
+          }
+          if (kCount) ctr.follows += popc64(__ballot(use));
+          if (!__any(fl)) continue;
+        }
+        // the neighbour among the leaves still to come: the retry joins its pass
+        const unsigned long long later = __ballot(lane > e && lane < ne && L.eid[lane & (kEntries - 1u)] == nb);
         if (later) {
           const unsigned long long fm = uniform_u64(L.emask[__builtin_ctzll(later)]);
-          if (fl && fnb == 0xFFFFFFFFu && !lane_bit(fm, lane)) {
-            fnb = nb;
-            fsrc = b;
+          if (fl && join == kNo && !lane_bit(fm, lane)) {
+            join = nb;
+            join_src = b;
             fl = false;
           }
         }
@@ -1189,7 +1150,6 @@ __device__ __forceinline__ void trace_segment_defer(const MeshView &m, f3 s, f3 
     }
   }
 }
-#endif
 
 // Trace job of one launch.  Modes: kModeHits (one BezierMesh::intersect per ray -> hits), kModeRefract
 // (one BezierLens::refract -> ray', status), kModeStage (the chain over lenses [0, count): refract(INSIDE)
@@ -1219,9 +1179,9 @@ struct TraceJob {
 template <int kMode, bool kFast, bool kCount>
 __global__ __launch_bounds__(kBlock) BZR_TRACE_ATTR void k_trace(LensSet lenses, TraceJob job,
                                                                  unsigned long long *__restrict__ counters) {
-  __shared__ TraceLds lds[kWaves];
+  __shared__ TraceLds<kMode> lds[kWaves];
   const uint32_t lane = threadIdx.x & 63u;
-  TraceLds &L = lds[threadIdx.x >> 6];
+  TraceLds<kMode> &L = lds[threadIdx.x >> 6];
   const uint32_t i = xcd_contiguous(blockIdx.x, gridDim.x) * kBlock + threadIdx.x;
   const uint32_t n = job.n;
   TraceCtr ctr;
@@ -1236,23 +1196,11 @@ __global__ __launch_bounds__(kBlock) BZR_TRACE_ATTR void k_trace(LensSet lenses,
     if (!__any(alive)) break;
     const MeshView &m = lenses.lens[k >> 1];
     unsigned long long best;
-#if BZR_TRACE_DEFER
-    trace_segment_defer<kFast, kCount>(m, s, d, alive, best, L, lane, ctr);
-#else
-    trace_segment<kFast, kCount>(m, s, d, alive, best, L, lane, ctr);
-#endif
+    trace_segment<kMode, kFast, kCount>(m, s, d, alive, best, L, lane, ctr);
     if (kCount) ctr.segments += popc64(__ballot(alive));
     Hit h = no_hit();
     uint32_t patch = 0xFFFFFFFFu;
-    if (best != ~0ull) {
-      h.t = L.hit[0][lane];
-      h.point = mk(L.hit[1][lane], L.hit[2][lane], L.hit[3][lane]);
-      h.cs = L.hit[4][lane];
-      h.bary = mk(L.hit[5][lane], L.hit[6][lane], L.hit[7][lane]);
-      h.normal = mk(L.hit[8][lane], L.hit[9][lane], L.hit[10][lane]);
-      h.what = kIntersect;
-      patch = __float_as_uint(L.hit[11][lane]);
-    }
+    if (best != ~0ull) h = winner(L, lane, patch);
     if (kMode == kModeHits) {
       if (alive) store_hit(job.hits, job.ld, i, h, patch);
     } else {
