@@ -12,9 +12,10 @@ A step = one frame: the whole chain over this rank's primary rays, inputs alread
 results bit-identical to the reference restatement (tests/test_gpu_parity.py).  N GPUs = N processes
 (torch.distributed over RCCL).  --scaling strong (default): the fixed side x side image is dealt to the
 ranks as 64x64 tiles round-robin (the north-star's 1->8 GPU scaling on a fixed 4096^2 grid); --scaling
-weak: the image grows to side x (side*N).  With --gather rays (default) each frame's results (28 B per
-primary) are gathered to rank 0 over RCCL inside the timed region, double-buffered so frame k's gather
-overlaps frame k+1's tracing.
+weak: the image grows to side x (side*N).  Each frame's results are gathered to rank 0 over RCCL inside
+the timed region, double-buffered so frame k's gather overlaps frame k+1's tracing: --gather image
+(default) the per-primary status + segment-count word (4 B; the final rays stay in each rank's HBM),
+--gather rays the final rays too (28 B per primary), --gather none nothing (tracing alone).
 
 Prints ONE JSON line on rank 0; fields are described in DESIGN.md (d).
 """
@@ -51,7 +52,8 @@ def parse():
     p.add_argument("--config", default="cfg4", choices=["cfg2", "cfg3", "cfg4", "cfg5"])
     p.add_argument("--side", type=int, default=0, help="override rays per image side")
     p.add_argument("--scaling", default="strong", choices=["strong", "weak"])
-    p.add_argument("--gather", default="rays", choices=["rays", "none"])
+    p.add_argument("--gather", default="image", choices=["image", "rays", "none"],
+                   help="what each frame sends to rank 0 when N > 1 (DESIGN.md (e) byte budget)")
     p.add_argument("--accel", default="bvh", choices=["bvh", "none"], help="none = brute-force scan (A/B)")
     p.add_argument("--pipeline", default="fused", choices=["fused", "staged", "auto"],
                    help="culled-path pipeline (include/bzr.h BZR_PIPELINE_*; same output bits): fused = one k_trace "
@@ -210,8 +212,10 @@ def main():
         out_seg = torch.empty(n, dtype=torch.int32, device=dev)
     else:
         hits = torch.empty((13, n), dtype=torch.float32, device=dev)
-    gather = world > 1 and a.gather == "rays"
-    rows = frame.PACKED_ROWS if chain else 13
+    gather = world > 1 and a.gather != "none"
+    # rays layout: the whole result (chain: 6 ray rows + status/segment word; intersect: the 13 hit rows);
+    # image layout: one word per primary (chain: status | segments << 8; intersect: the hit's `what` row)
+    rows = 1 if a.gather == "image" else (frame.PACKED_ROWS if chain else 13)
     # double-buffered frame gather: frame k's packed results travel to rank 0 (RCCL, its own stream)
     # while frame k+1 is traced; a buffer is refilled only after its previous gather completed.  Buffers
     # hold the largest rank's share (strong scaling may deal one tile fewer to some ranks).
@@ -237,6 +241,8 @@ def main():
                 pending[slot].wait()
             if chain:
                 frame.pack(out_rays, out_status, out_seg, packed[slot])
+            elif rows == 1:
+                packed[slot][0, :n].copy_(hits[11])
             else:
                 packed[slot][:, :n].copy_(hits)
             pending[slot] = frame.gather(packed[slot], world, rank, gather_list=gather_lists[slot], async_op=True)
@@ -352,7 +358,8 @@ def main():
                 "segments_per_step": seg_total,
                 "patches": n_patch,
                 "parallelism": f"64x64 image tiles round-robin over {world} rank(s), {a.scaling} scaling"
-                               + (", RCCL gather of every frame to rank 0 (overlapped with the next frame)" if gather else ""),
+                               + (f", RCCL gather of every frame to rank 0 (overlapped with the next frame): "
+                                  f"{rows * 4} B per primary ({a.gather})" if gather else ""),
                 "pipeline": a.pipeline,
                 "scan": "BVH-culled (bit-identical to brute force)" if a.accel == "bvh" else "brute force",
                 "numerics": "parity: bit-identical to the CPU oracle" if a.mode == "parity" else

@@ -20,7 +20,7 @@ def free_port():
         return s.getsockname()[1]
 
 
-def worker(rank, world, port, width, height, patches, result_path):
+def worker(rank, world, port, width, height, patches, result_path, layout="rays"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -29,13 +29,17 @@ def worker(rank, world, port, width, height, patches, result_path):
         cfg = CONFIGS["cfg2"]
         rows, cols, rays = frame.rank_rays(cfg, rank, world, width, height)
         o, s, g = pyoracle.trace_chain([patches], [1.3], rays, threads=2)
-        packed = torch.zeros((frame.PACKED_ROWS, frame.padded_count(world, width, height)), dtype=torch.float32)
+        rows_packed = frame.PACKED_ROWS if layout == "rays" else frame.IMAGE_ROWS
+        packed = torch.zeros((rows_packed, frame.padded_count(world, width, height)), dtype=torch.float32)
         frame.pack(torch.from_numpy(o), torch.from_numpy(s.view(np.int32)), torch.from_numpy(g.view(np.int32)), packed)
         glist = [torch.empty_like(packed) for _ in range(world)] if rank == 0 else None
         parts = frame.gather(packed, world, rank, gather_list=glist)
         if rank == 0:
             r, st, sg = frame.assemble(parts, cfg, world, width, height)
-            np.savez(result_path, rays=r, status=st, seg=sg)
+            if r is None:
+                np.savez(result_path, status=st, seg=sg)
+            else:
+                np.savez(result_path, rays=r, status=st, seg=sg)
     finally:
         dist.destroy_process_group()
 
@@ -57,3 +61,21 @@ def test_sharded_frame_equals_single_process(bzr, orc, world, scaling, tmp_path)
     assert np.array_equal(got["status"][flat], s) and np.array_equal(got["seg"][flat], g)
     assert np.array_equal(got["rays"][:, flat].view(np.uint32), o.view(np.uint32))
     assert got["seg"].sum() > width * height  # refracted segments were traced
+
+
+def test_image_layout_gather(bzr, orc, tmp_path):
+    """bench.py's default multi-GPU gather (--gather image): only the status/segment word per primary
+    reaches rank 0 (4 B instead of 28 B); the assembled image equals the single-process trace's."""
+    cfg = CONFIGS["cfg2"]
+    patches = bzr.TriMesh().make_ellipsoid(32, 16, (1, 4, 2)).translate((10, 0, 0)).standardize().bezier_patches()
+    world, width, height = 3, 128, 128
+    out = tmp_path / "image.npz"
+    mp.start_processes(worker, args=(world, free_port(), width, height, patches, str(out), "image"), nprocs=world,
+                       join=True, start_method="spawn")
+    got = np.load(out)
+    assert "rays" not in got.files
+    rows, cols, rays = frame.rank_rays(cfg, 0, 1, width, height)
+    o, s, g = orc.trace_chain([patches], [1.3], rays)
+    flat = rows * width + cols
+    assert np.array_equal(got["status"][flat], s) and np.array_equal(got["seg"][flat], g)
+    assert (got["status"] != 0).any()
