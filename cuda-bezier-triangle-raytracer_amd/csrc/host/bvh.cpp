@@ -111,19 +111,28 @@ Box gate_region_box(const float *rec, double s_max, Region *region = nullptr) {
     ext += 2.0 * normd(q[k]);
   }
   if (!std::isfinite(ext)) return all;
-  double X = ext;  // bound on |x| over P (every vertex of P is within sum |q_k| (1 + 2 slack))
-  // kappa = gamma_3 max_i l1_i sum_k |q_k|_inf (gamma_3 = 3.0000002 u, u = 2^-24): a passing float p has
-  // fl(M_i p) in [0,1], so |b_k| = |M_k p| <= 1 + gamma_3 l1 |p|_inf and |p|_inf <= sum_k |q_k|_inf |b_k|;
-  // for kappa < 1/2 that gives |p|_inf <= 2 sum_k |q_k| <= X, and slack_i = kSlack (l1_i X + 1) >=
-  // gamma_3 l1_i X is a proven allowance.  For kappa >= 1/2 the float gate's rounding is not bounded this
-  // way (the rows of M are nearly parallel to the normal: fl(M p) is rounding noise near the plane,
-  // SURVEY.md 0.4); those patches keep round 1's construction and allowance (kRel), and their culling
-  // is checked empirically (tests/test_gpu_parity.py culled == brute force).
-  double l1max = 0.0, qsum = 0.0;
-  for (int i = 0; i < 3; ++i) l1max = std::max(l1max, std::fabs(row[i][0]) + std::fabs(row[i][1]) + std::fabs(row[i][2]));
-  for (int k = 0; k < 3; ++k) qsum += std::max({std::fabs(q[k][0]), std::fabs(q[k][1]), std::fabs(q[k][2])});
-  const double kappa = 3.0000002 / 16777216.0 * l1max * qsum;
-  const double kslack = kappa < 0.5 ? kSlack : kRel;
+  // kappa = gamma_3 sum_k |q_k|_inf l1_k (gamma_3 = 3.0000002 u, u = 2^-24; l1_k = |M_k|_1): a passing
+  // float p has fl(M_k p) in [0,1], so |b_k| = |M_k p| <= 1 + gamma_3 l1_k |p|_inf and |p|_inf <=
+  // sum_k |q_k|_inf |b_k| <= S + kappa |p|_inf (S = sum_k |q_k|_inf); for kappa < 1 that gives
+  // |p|_inf <= S / (1 - kappa) =: X (at least ext, which bounds P's vertices), and slack_i =
+  // kSlack (l1_i X + 1) >= gamma_3 l1_i X is a proven allowance.  For kappa >= 1 the float gate's rounding
+  // is not bounded this way (the rows of M are nearly parallel to the normal: fl(M p) is rounding noise
+  // near the plane); those patches keep round 1's allowance (kRel, X = ext), and their
+  // culling is checked empirically (tests/test_culling_conservative.py, tests/test_gpu_parity.py culled
+  // == brute force).
+  double qsum = 0.0, kappa = 0.0;
+  for (int k = 0; k < 3; ++k) {
+    const double qk = std::max({std::fabs(q[k][0]), std::fabs(q[k][1]), std::fabs(q[k][2])});
+    qsum += qk;
+    kappa += 3.0000002 / 16777216.0 * qk * (std::fabs(row[k][0]) + std::fabs(row[k][1]) + std::fabs(row[k][2]));
+  }
+#ifndef BZR_BVH_KAPPA_PROVEN
+#define BZR_BVH_KAPPA_PROVEN 1.0
+#endif
+  const bool proven = kappa < BZR_BVH_KAPPA_PROVEN;
+  const double X = proven ? std::max(ext, qsum / (1.0 - kappa)) : ext;
+  if (!std::isfinite(X)) return all;
+  const double kslack = proven ? kSlack : kRel;
   double slack[3];
   for (int i = 0; i < 3; ++i) {
     double l1 = std::fabs(row[i][0]) + std::fabs(row[i][1]) + std::fabs(row[i][2]);
