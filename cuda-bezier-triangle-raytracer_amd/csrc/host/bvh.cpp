@@ -111,32 +111,64 @@ Box gate_region_box(const float *rec, double s_max, Region *region = nullptr) {
     ext += 2.0 * normd(q[k]);
   }
   if (!std::isfinite(ext)) return all;
-  // kappa = gamma_3 sum_k |q_k|_inf l1_k (gamma_3 = 3.0000002 u, u = 2^-24; l1_k = |M_k|_1): a passing
-  // float p has fl(M_k p) in [0,1], so |b_k| = |M_k p| <= 1 + gamma_3 l1_k |p|_inf and |p|_inf <=
-  // sum_k |q_k|_inf |b_k| <= S + kappa |p|_inf (S = sum_k |q_k|_inf); for kappa < 1 that gives
-  // |p|_inf <= S / (1 - kappa) =: X (at least ext, which bounds P's vertices), and slack_i =
-  // kSlack (l1_i X + 1) >= gamma_3 l1_i X is a proven allowance.  For kappa >= 1 the float gate's rounding
-  // is not bounded this way (the rows of M are nearly parallel to the normal: fl(M p) is rounding noise
-  // near the plane); those patches keep round 1's allowance (kRel, X = ext), and their
-  // culling is checked empirically (tests/test_culling_conservative.py, tests/test_gpu_parity.py culled
-  // == brute force).
-  double qsum = 0.0, kappa = 0.0;
-  for (int k = 0; k < 3; ++k) {
-    const double qk = std::max({std::fabs(q[k][0]), std::fabs(q[k][1]), std::fabs(q[k][2])});
-    qsum += qk;
-    kappa += 3.0000002 / 16777216.0 * qk * (std::fabs(row[k][0]) + std::fabs(row[k][1]) + std::fabs(row[k][2]));
+  // Where can a passing float p lie?  fl(M_k p) = M_k p + e_k with |e_k| <= gamma_3 sum_l |M_kl| |p_l|
+  // (gamma_3 = 3.0000002 u, u = 2^-24), and the gate needs fl(M p) in [0,1]^3.  With Q = M^-1,
+  // p = Q (b - e) for some b in [0,1]^3, so componentwise |p| <= |Q| 1 + G |p| with G = gamma_3 |Q| |M|.
+  // When I - G is a nonsingular M-matrix (spectral radius of G < 1; checked by its leading principal
+  // minors) that gives |p| <= P = (I - G)^-1 |Q| 1, hence |e_k| <= gamma_3 sum_l |M_kl| P_l, and
+  // slack_k = kSlack (sum_l |M_kl| P_l + 1) (kSlack = 2.7 gamma_3) is a proven allowance; X = max(max P,
+  // ext) bounds |p|_inf.  |Q| is the double-precision inverse widened by its residual.  Otherwise (the
+  // rounding-dominated patches: the rows of M nearly parallel to the normal, fl(M p) is rounding noise
+  // near the plane) the patch keeps round 1's allowance kRel (l1_k ext + 1), checked
+  // empirically (tests/test_culling_conservative.py, tests/test_gpu_parity.py culled == brute force).
+  const double g3 = 3.0000002 / 16777216.0;
+  double rn = 0.0;  // max column sum of |I - M Q~|
+  for (int j = 0; j < 3; ++j) {
+    double cs = 0.0;
+    for (int i = 0; i < 3; ++i) {
+      double mq = 0.0;
+      for (int k = 0; k < 3; ++k) mq += row[i][k] * q[j][k];
+      cs += std::fabs((i == j ? 1.0 : 0.0) - mq);
+    }
+    rn = std::max(rn, cs);
   }
-#ifndef BZR_BVH_KAPPA_PROVEN
-#define BZR_BVH_KAPPA_PROVEN 1.0
-#endif
-  const bool proven = kappa < BZR_BVH_KAPPA_PROVEN;
-  const double X = proven ? std::max(ext, qsum / (1.0 - kappa)) : ext;
-  if (!std::isfinite(X)) return all;
-  const double kslack = proven ? kSlack : kRel;
-  double slack[3];
+  double qa[3][3];  // |Q| bound, [i][k] = row i, column k
   for (int i = 0; i < 3; ++i) {
-    double l1 = std::fabs(row[i][0]) + std::fabs(row[i][1]) + std::fabs(row[i][2]);
-    slack[i] = kslack * (l1 * X + 1.0);
+    const double rmax = std::max({std::fabs(q[0][i]), std::fabs(q[1][i]), std::fabs(q[2][i])});
+    for (int k = 0; k < 3; ++k) qa[i][k] = std::fabs(q[k][i]) * (1.0 + 1e-12) + 4.0 * rn * rmax;
+  }
+  double A[3][3];  // I - G
+  for (int i = 0; i < 3; ++i)
+    for (int l = 0; l < 3; ++l) {
+      double gil = 0.0;
+      for (int k = 0; k < 3; ++k) gil += qa[i][k] * std::fabs(row[k][l]);
+      A[i][l] = (i == l ? 1.0 : 0.0) - g3 * gil * (1.0 + 1e-12);
+    }
+  const double m1 = A[0][0], m2 = A[0][0] * A[1][1] - A[0][1] * A[1][0];
+  const double m3 = A[0][0] * (A[1][1] * A[2][2] - A[1][2] * A[2][1]) - A[0][1] * (A[1][0] * A[2][2] - A[1][2] * A[2][0]) +
+                    A[0][2] * (A[1][0] * A[2][1] - A[1][1] * A[2][0]);
+  double P[3] = {0.0, 0.0, 0.0};
+  bool proven = rn < 1e-4 && m1 > 1e-9 && m2 > 1e-9 && m3 > 1e-9;
+  if (proven) {  // P = A^-1 (|Q| 1) by the adjugate (A is a Z-matrix with positive leading minors: an
+                 // M-matrix, so A^-1 >= 0; |.| only guards the rounding of entries that are ~0)
+    const double qs[3] = {qa[0][0] + qa[0][1] + qa[0][2], qa[1][0] + qa[1][1] + qa[1][2], qa[2][0] + qa[2][1] + qa[2][2]};
+    for (int i = 0; i < 3 && proven; ++i) {
+      double acc = 0.0;
+      for (int l = 0; l < 3; ++l) {
+        const int r1 = (l + 1) % 3, r2 = (l + 2) % 3, c1 = (i + 1) % 3, c2 = (i + 2) % 3;
+        acc += std::fabs((A[r1][c1] * A[r2][c2] - A[r1][c2] * A[r2][c1]) / m3) * qs[l];  // |(A^-1)[i][l]| (|Q| 1)_l
+      }
+      P[i] = acc * (1.0 + 1e-9);
+      if (!std::isfinite(P[i])) proven = false;
+    }
+  }
+  const double X = proven ? std::max({ext, P[0], P[1], P[2]}) : ext;
+  if (!std::isfinite(X)) return all;
+  double slack[3];
+  for (int k = 0; k < 3; ++k) {
+    const double l1 = std::fabs(row[k][0]) + std::fabs(row[k][1]) + std::fabs(row[k][2]);
+    slack[k] = proven ? kSlack * (std::fabs(row[k][0]) * P[0] + std::fabs(row[k][1]) * P[1] + std::fabs(row[k][2]) * P[2] + 1.0)
+                      : kRel * (l1 * X + 1.0);
   }
   const double eps = kRel * (X + s_max);  // off-plane distance of the float plane point
   std::vector<d3> pts;
