@@ -30,21 +30,35 @@ double dotd(d3 a, d3 b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
 d3 crossd(d3 a, d3 b) { return {a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]}; }
 double normd(d3 a) { return std::sqrt(dotd(a, a)); }
 
-// Rounding allowances of the float planar gate (u = 2^-24; X bounds |x| over the region, s_max |origin|):
-//   kRel    the plane slab eps and the ray-point / slab-test pad: the float ray/plane point p lies within
-//           ~18 u (X + s_max) of the plane (fl(n.s), fl(d.n) and the division's rounding, the last scaled
-//           by t: off-plane distance ~ t * err(d.n) <= 3 sqrt3 u |p - s|) -- 2^-18 = 64 u is 3.5x that
-//   kSlack  the barycentric slack: fl(M_i . p) differs from M_i . p by at most gamma_3 sum_j |M_ij p_j|
-//           <= 3.0000002 u l1_i X -- 2^-21 = 8 u is 2.7x that.  (Ill-conditioned M makes l1 large: this
-//           term sets the in-plane size of the wide patches' regions.)
-#ifndef BZR_BVH_KREL_LOG2
-#define BZR_BVH_KREL_LOG2 18
+// Rounding allowances of the float planar gate (u = 2^-24; X bounds |x|_inf over the region, s_max
+// |origin|_inf; n, c the record's plane, nu = |n|).  plane_ray computes D^ = fl(n.s), t^ = fl(fl(c - D^) /
+// fl(d.n)) and p^ = fl(s + fl(d t^)).  With p~ = s + d t^ (exact), n.p~ - c = (n.s - D^) + (c - D^) d12 -
+// eta t^ (|d12| <= gamma_2, |eta| <= gamma_3 sum |d_i n_i|), and |p^_i - p~_i| <= u (|d_i t^| + |p^_i|);
+// bounding each term with |s| <= s_max, |p^|, |p~ - s| <= sqrt3 (X + s_max) gives
+//   off-plane distance |n.p^ - c| / nu <= u (sqrt3 (9 s_max + 5 X) + 2 |c| / nu) <= 16 u (X + s_max)
+//   distance of p^ from the ray line    <= |p^ - p~| <= 2 sqrt3 u (X + s_max)
+// (measured over 2e5 random and grazing rays on cfg5's patches: at most 4.6 u and 1.6 u -- tests/
+// test_culling_conservative.py pins both).  Allowances:
+//   kEps    the plane slab: 24 u (X + s_max), 1.5x the bound
+//   kPad    the box padding for the ray-line distance plus the float slab test's own rounding
+//           (t = fma(lo, 1/d, -s/d): ~4 u (X + s_max) in space): 16 u (X + s_max), 2x the sum
+//   kSlack  the barycentric slack: fl(M_k p) differs from M_k p by at most gamma_3 sum_l |M_kl| |p_l|
+//           (gamma_3 = 3.0000002 u) -- 2^-21 = 8 u is 2.7x that (proven allowance, see gate_region_box)
+//   kRound1 round 1's allowance, 2^-18 = 64 u, kept for the barycentric slack of the rounding-dominated
+//           patches, whose gate no bound covers (checked empirically)
+#ifndef BZR_BVH_EPS_U
+#define BZR_BVH_EPS_U 24.0
+#endif
+#ifndef BZR_BVH_PAD_U
+#define BZR_BVH_PAD_U 16.0
 #endif
 #ifndef BZR_BVH_KSLACK_LOG2
 #define BZR_BVH_KSLACK_LOG2 21
 #endif
-constexpr double kRel = 1.0 / (1 << BZR_BVH_KREL_LOG2);
+constexpr double kEps = BZR_BVH_EPS_U / 16777216.0;
+constexpr double kPad = BZR_BVH_PAD_U / 16777216.0;
 constexpr double kSlack = 1.0 / (1 << BZR_BVH_KSLACK_LOG2);
+constexpr double kRound1 = 1.0 / (1 << 18);
 
 // Clip convex polygon `poly` (plane points) to { x : g.x + h >= 0 }.
 std::vector<d3> clip(std::vector<d3> const &poly, d3 g, double h) {
@@ -119,7 +133,7 @@ Box gate_region_box(const float *rec, double s_max, Region *region = nullptr) {
   // slack_k = kSlack (sum_l |M_kl| P_l + 1) (kSlack = 2.7 gamma_3) is a proven allowance; X = max(max P,
   // ext) bounds |p|_inf.  |Q| is the double-precision inverse widened by its residual.  Otherwise (the
   // rounding-dominated patches: the rows of M nearly parallel to the normal, fl(M p) is rounding noise
-  // near the plane) the patch keeps round 1's allowance kRel (l1_k ext + 1), checked
+  // near the plane) the patch keeps round 1's allowance kRound1 (l1_k ext + 1), checked
   // empirically (tests/test_culling_conservative.py, tests/test_gpu_parity.py culled == brute force).
   const double g3 = 3.0000002 / 16777216.0;
   double rn = 0.0;  // max column sum of |I - M Q~|
@@ -168,9 +182,9 @@ Box gate_region_box(const float *rec, double s_max, Region *region = nullptr) {
   for (int k = 0; k < 3; ++k) {
     const double l1 = std::fabs(row[k][0]) + std::fabs(row[k][1]) + std::fabs(row[k][2]);
     slack[k] = proven ? kSlack * (std::fabs(row[k][0]) * P[0] + std::fabs(row[k][1]) * P[1] + std::fabs(row[k][2]) * P[2] + 1.0)
-                      : kRel * (l1 * X + 1.0);
+                      : kRound1 * (l1 * X + 1.0);
   }
-  const double eps = kRel * (X + s_max);  // off-plane distance of the float plane point
+  const double eps = kEps * (X + s_max);  // off-plane distance of the float plane point
   std::vector<d3> pts;
   // the initial square must contain the whole slab slice of the slack-inflated parallelepiped
   double qn = 0.0, smax_slack = std::max({slack[0], slack[1], slack[2]});
@@ -211,7 +225,7 @@ Box gate_region_box(const float *rec, double s_max, Region *region = nullptr) {
     bx.empty = true;
     return bx;
   }
-  double pad = kRel * (X + s_max) + 1e-6;  // ray-point and slab-test rounding
+  double pad = kPad * (X + s_max) + 1e-6;  // ray-line distance of the plane point and slab-test rounding
   if (region) region->pad = pad;
   for (int a = 0; a < 3; ++a) {
     bx.lo[a] = static_cast<float>(std::nextafter(lo[a] - pad, -HUGE_VAL));

@@ -259,3 +259,43 @@ def test_rounding_dominated_counts(bzr, cfg_name, expect):
     cfg1/cfg2/cfg3's or the north-star lens's (cfg4), 126 of cfg5's 301 056."""
     patches = build_lens(bzr.TriMesh, CONFIGS[cfg_name].lenses[0]).bezier_patches()
     assert len(rounding_dominated(patches)) == expect
+
+
+@pytest.mark.parametrize("cfg_name", ["cfg2", "cfg5"])
+def test_plane_point_rounding_within_derived_bounds(bzr, cfg_name):
+    """bvh.cpp's slab and padding allowances rest on two derived bounds for the float ray/plane point p^
+    of the planar gate (plane_ray, reference/3dGeomUtil.h:279-296, evaluated here in float32 in the
+    kernel's operation order): off-plane distance <= 16 u (|p^| + |s|) and distance from the ray line
+    <= 2 sqrt3 u (|p^| + |s|) (inf-norms, u = 2^-24).  Random, aimed and grazing rays on the config's
+    patches must stay within them; the allowances themselves are 1.5x and 2x larger."""
+    f, u = np.float32, 2.0 ** -24
+    p = build_lens(bzr.TriMesh, CONFIGS[cfg_name].lenses[0]).bezier_patches()
+    rng = np.random.default_rng(23)
+    m = 200_000
+    idx = rng.integers(0, len(p), m)
+    n, c = p[idx, 0:3].astype(f), p[idx, 3].astype(f)
+    cp = p[idx, 19:22].astype(np.float64)
+    s = (cp + rng.uniform(-1, 1, (m, 3)) * rng.choice([1.0, 10.0, 80.0], (m, 1))).astype(f)
+    tgt = cp + rng.normal(size=(m, 3)) * 0.3
+    d = tgt - s.astype(np.float64)
+    graze = rng.random(m) < 0.3  # project a third of the directions almost into the plane
+    nd = n.astype(np.float64) / np.linalg.norm(n.astype(np.float64), axis=1, keepdims=True)
+    d[graze] -= (d[graze] * nd[graze]).sum(1, keepdims=True) * nd[graze] * (1 - rng.uniform(1e-5, 1e-3, (graze.sum(), 1)))
+    d = (d / np.linalg.norm(d, axis=1, keepdims=True)).astype(f)
+
+    def dot(a, b):
+        return (a[:, 0] * b[:, 0] + (a[:, 1] * b[:, 1] + a[:, 2] * b[:, 2])).astype(f)
+
+    cs = dot(d, n)
+    with np.errstate(all="ignore"):
+        t = ((c - dot(n, s)).astype(f) / cs).astype(f)
+        ph = (s + (d * t[:, None]).astype(f)).astype(f)
+    ok = (np.abs(cs) >= f(1e-5)) & (t > 0) & np.isfinite(ph).all(axis=1)
+    assert ok.sum() > m // 2 and (ok & graze).sum() > m // 10
+    p64, s64, d64, n64 = ph[ok].astype(np.float64), s[ok].astype(np.float64), d[ok].astype(np.float64), n[ok].astype(np.float64)
+    scale = u * (np.abs(p64).max(1) + np.abs(s64).max(1))
+    off = np.abs((n64 * p64).sum(1) - c[ok].astype(np.float64)) / np.linalg.norm(n64, axis=1)
+    w = p64 - s64
+    line = np.linalg.norm(w - (w * d64).sum(1, keepdims=True) * d64 / (d64 * d64).sum(1, keepdims=True), axis=1)
+    assert (off <= 16 * scale).all(), (off / scale).max()
+    assert (line <= 2 * np.sqrt(3) * scale).all(), (line / scale).max()
