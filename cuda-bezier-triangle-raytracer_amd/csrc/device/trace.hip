@@ -1176,13 +1176,19 @@ struct TraceJob {
 #else
 #define BZR_TRACE_ATTR
 #endif
+// Threads per k_trace block (BZR_TRACE_BLOCK): its waves share nothing but the CU, so one-wave blocks let
+// a finished wave be replaced at once (waves run 1-4 segments; 64 vs 256: cfg4 -3 %, cfg5 -7 %).
+#ifndef BZR_TRACE_BLOCK
+#define BZR_TRACE_BLOCK 64
+#endif
+constexpr int kTraceBlock = BZR_TRACE_BLOCK, kTraceWaves = kTraceBlock / 64;
 template <int kMode, bool kFast, bool kCount>
-__global__ __launch_bounds__(kBlock) BZR_TRACE_ATTR void k_trace(LensSet lenses, TraceJob job,
-                                                                 unsigned long long *__restrict__ counters) {
-  __shared__ TraceLds<kMode> lds[kWaves];
+__global__ __launch_bounds__(kTraceBlock) BZR_TRACE_ATTR void k_trace(LensSet lenses, TraceJob job,
+                                                                      unsigned long long *__restrict__ counters) {
+  __shared__ TraceLds<kMode> lds[kTraceWaves];
   const uint32_t lane = threadIdx.x & 63u;
   TraceLds<kMode> &L = lds[threadIdx.x >> 6];
-  const uint32_t i = xcd_contiguous(blockIdx.x, gridDim.x) * kBlock + threadIdx.x;
+  const uint32_t i = xcd_contiguous(blockIdx.x, gridDim.x) * kTraceBlock + threadIdx.x;
   const uint32_t n = job.n;
   TraceCtr ctr;
   bool alive = i < n;
@@ -1237,7 +1243,7 @@ __global__ __launch_bounds__(kBlock) BZR_TRACE_ATTR void k_trace(LensSet lenses,
         mine = v[k];
         which = id[k];
       }
-    const uint32_t rep = (blockIdx.x * kWaves + (threadIdx.x >> 6)) % kCounterReplicas;
+    const uint32_t rep = (blockIdx.x * kTraceWaves + (threadIdx.x >> 6)) % kCounterReplicas;
     if (mine) atomicAdd(&counters[(size_t)rep * BZR_COUNTER_COUNT + which], (unsigned long long)mine);
   }
 }
@@ -1543,13 +1549,14 @@ template <int kMode>
 bzr_status run_fused(bzr_ctx *ctx, const LensSet &set, const TraceJob &job, uint32_t flags) {
   if (job.n == 0) return BZR_OK;
   const bool fast = use_fast(flags), count = ctx->counting && ctx->counters;
-  const dim3 grid(grid_for(job.n));
+  const dim3 grid((job.n + kTraceBlock - 1) / kTraceBlock), block(kTraceBlock);
+  auto go = [&](auto kernel) { launch_on(ctx, ctx->stream, block, BZR_KERNEL_TRACE, kernel, grid, set, job, ctx->counters); };
   if (fast) {
-    if (count) launch(ctx, BZR_KERNEL_TRACE, k_trace<kMode, true, true>, grid, set, job, ctx->counters);
-    else launch(ctx, BZR_KERNEL_TRACE, k_trace<kMode, true, false>, grid, set, job, ctx->counters);
+    if (count) go(k_trace<kMode, true, true>);
+    else go(k_trace<kMode, true, false>);
   } else {
-    if (count) launch(ctx, BZR_KERNEL_TRACE, k_trace<kMode, false, true>, grid, set, job, ctx->counters);
-    else launch(ctx, BZR_KERNEL_TRACE, k_trace<kMode, false, false>, grid, set, job, ctx->counters);
+    if (count) go(k_trace<kMode, false, true>);
+    else go(k_trace<kMode, false, false>);
   }
   BZR_HIP(hipGetLastError());
   return BZR_OK;
