@@ -63,12 +63,14 @@ def test_sharded_frame_equals_single_process(bzr, orc, world, scaling, tmp_path)
     assert got["seg"].sum() > width * height  # refracted segments were traced
 
 
-def test_image_layout_gather(bzr, orc, tmp_path):
+@pytest.mark.parametrize("world,side", [(3, 128), (8, 256)])
+def test_image_layout_gather(bzr, orc, tmp_path, world, side):
     """bench.py's default multi-GPU gather (--gather image): only the status/segment word per primary
-    reaches rank 0 (4 B instead of 28 B); the assembled image equals the single-process trace's."""
+    reaches rank 0 (4 B instead of 28 B); the assembled image equals the single-process trace's.  World 8
+    is the driver's SCALE run's largest rank count (a 256^2 image: 16 tiles, 2 per rank)."""
     cfg = CONFIGS["cfg2"]
     patches = bzr.TriMesh().make_ellipsoid(32, 16, (1, 4, 2)).translate((10, 0, 0)).standardize().bezier_patches()
-    world, width, height = 3, 128, 128
+    width = height = side
     out = tmp_path / "image.npz"
     mp.start_processes(worker, args=(world, free_port(), width, height, patches, str(out), "image"), nprocs=world,
                        join=True, start_method="spawn")
