@@ -1380,13 +1380,16 @@ bool use_fast(uint32_t flags) { return (flags & BZR_MODE_FAST) != 0; }
 // Culled-path pipeline for a call of n rays over meshes of at most nb patches (include/bzr.h): forced by
 // BZR_PIPELINE_STAGED / BZR_PIPELINE_FUSED, otherwise fused for dense batches (rays per patch >= 2048:
 // cfg4 at 4096^2 has 5461 and a wave's 64 rays meet ~2 patches per segment; cfg2 at 1024^2 has 341 and
-// the staged path is 1.5x faster there) and for large meshes (>= 2^16 patches: the walk dominates both
-// pipelines and the fused one saves the per-pair traffic -- cfg5, 301 056 patches, 1.1x), DESIGN.md (a).
-constexpr uint64_t kFusedRaysPerPatch = 2048, kFusedPatches = 1u << 16;
+// the staged path is 1.5x faster there) and for large meshes with >= 128 rays per patch (>= 2^16
+// patches: the walk dominates both pipelines and the fused one saves the per-pair traffic -- cfg5,
+// 301 056 patches: 1.1x at 8192^2, 223 rays per patch; at 4096^2, 56 per patch, staged is 1.06x faster),
+// DESIGN.md (a).
+constexpr uint64_t kFusedRaysPerPatch = 2048, kFusedPatches = 1u << 16, kFusedLargeRaysPerPatch = 128;
 bool use_staged(uint32_t flags, uint64_t n, uint64_t nb) {
   if (flags & BZR_PIPELINE_STAGED) return true;
   if (flags & BZR_PIPELINE_FUSED) return false;
-  return n < kFusedRaysPerPatch * nb && nb < kFusedPatches;
+  const bool dense = n >= kFusedRaysPerPatch * nb, large = nb >= kFusedPatches && n >= kFusedLargeRaysPerPatch * nb;
+  return !(dense || large);
 }
 // BZR_MODE_FAST runs on the culled pipeline's kernels only; the brute-force scan is the parity reference.
 bzr_status check_flags(uint32_t flags) {
