@@ -97,6 +97,7 @@ struct bzr_ctx {
   hipEvent_t handoff = nullptr;  // orders a new stream after the previous one (bzr_ctx_set_stream)
   double ms[BZR_KERNEL_COUNT] = {};
   uint32_t calls[BZR_KERNEL_COUNT] = {};
+  uint32_t chunk_cap = 0;                // staged-path rays per chunk (0: not yet sized, chunk_for)
   bool counting = false;                 // work counters (bzr_ctx_counters)
   unsigned long long *counters = nullptr;  // device [BZR_COUNTER_COUNT]
 };
@@ -1379,17 +1380,13 @@ bool use_scan(uint32_t flags) { return (flags & BZR_ACCEL_NONE) != 0; }
 bool use_fast(uint32_t flags) { return (flags & BZR_MODE_FAST) != 0; }
 // Culled-path pipeline for a call of n rays over meshes of at most nb patches (include/bzr.h): forced by
 // BZR_PIPELINE_STAGED / BZR_PIPELINE_FUSED, otherwise fused for dense batches (rays per patch >= 2048:
-// cfg4 at 4096^2 has 5461 and a wave's 64 rays meet ~2 patches per segment; cfg2 at 1024^2 has 341 and
-// the staged path is 1.5x faster there) and for large meshes with >= 128 rays per patch (>= 2^16
-// patches: the walk dominates both pipelines and the fused one saves the per-pair traffic -- cfg5,
-// 301 056 patches: 1.1x at 8192^2, 223 rays per patch; at 4096^2, 56 per patch, staged is 1.06x faster),
-// DESIGN.md (a).
-constexpr uint64_t kFusedRaysPerPatch = 2048, kFusedPatches = 1u << 16, kFusedLargeRaysPerPatch = 128;
+// cfg4 at 4096^2 has 5461 and a wave's 64 rays meet ~2 patches per segment, fused 1.2x faster; cfg2 at
+// 1024^2 has 341 and staged is 1.5x faster there; cfg5 has 56-223, staged 1.3x), DESIGN.md (a).
+constexpr uint64_t kFusedRaysPerPatch = 2048;
 bool use_staged(uint32_t flags, uint64_t n, uint64_t nb) {
   if (flags & BZR_PIPELINE_STAGED) return true;
   if (flags & BZR_PIPELINE_FUSED) return false;
-  const bool dense = n >= kFusedRaysPerPatch * nb, large = nb >= kFusedPatches && n >= kFusedLargeRaysPerPatch * nb;
-  return !(dense || large);
+  return n < kFusedRaysPerPatch * nb;
 }
 // BZR_MODE_FAST runs on the culled pipeline's kernels only; the brute-force scan is the parity reference.
 bzr_status check_flags(uint32_t flags) {
@@ -1499,9 +1496,28 @@ bzr_status ensure_work(bzr_ctx *ctx, uint32_t chunk, uint32_t nb, Work &w) {
   return BZR_OK;
 }
 
-// Chunk size of the culled path: bounds the workspace (~1.5 KB per ray) for very large batches.
-constexpr uint32_t kChunk = 1u << 20;
-uint32_t chunk_for(uint32_t n) { return n < kChunk ? n : kChunk; }
+// Rays per chunk of the staged path, whose workspace is ~3.7 KB per ray: at most
+// 2^BZR_CHUNK_LOG2 (8M rays, ~31 GB) and at most what a quarter of the device's free memory holds (at the
+// context's first staged call), with the
+// batch split into equal chunks (rounded to whole waves).  Measured on cfg5 (67M rays): 1M-ray chunks
+// 28.3 ms per frame, 4M 21.4, 8M 20.0, 16M 20.0 -- small chunks leave the kernels short of waves.
+#ifndef BZR_CHUNK_LOG2
+#define BZR_CHUNK_LOG2 23
+#endif
+constexpr uint32_t kChunk = 1u << BZR_CHUNK_LOG2;
+constexpr size_t kWorkBytesPerRay = (size_t)kMaxCand * (4 + 4 + 48 + 32 + 4) + 16;
+uint32_t chunk_for(bzr_ctx *ctx, uint64_t n) {
+  if (!ctx->chunk_cap) {
+    size_t free_b = 0, total_b = 0;
+    uint64_t cap = kChunk;
+    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b)
+      cap = std::min<uint64_t>(cap, std::max<uint64_t>(free_b / 4 / kWorkBytesPerRay / 64 * 64, 64));
+    ctx->chunk_cap = static_cast<uint32_t>(cap);
+  }
+  const uint64_t cap = ctx->chunk_cap, pieces = (n + cap - 1) / cap;
+  if (pieces <= 1) return static_cast<uint32_t>(std::max<uint64_t>(n, 1));
+  return static_cast<uint32_t>(std::min<uint64_t>(cap, ((n + pieces - 1) / pieces + 63) / 64 * 64));
+}
 
 // One BezierMesh::intersect per ray of rays [off, off + n) (+ refraction, per kMode).
 template <int kMode, bool kFast>
@@ -1856,7 +1872,7 @@ extern "C" bzr_status bzr_intersect(bzr_ctx *ctx, const bzr_mesh *mesh, const fl
     if (bzr_status s = run_fused<kModeHits>(ctx, single_lens(mv), job, flags)) return s;
   } else {
     Work w;
-    const uint32_t ch = chunk_for(n);
+    const uint32_t ch = chunk_for(ctx, n);
     if (bzr_status s = ensure_work(ctx, ch, mesh->n, w)) return s;
     Out o{};
     o.hits = d_hits;
@@ -1950,7 +1966,7 @@ extern "C" bzr_status bzr_refract(bzr_ctx *ctx, const bzr_mesh *mesh, float ri, 
     if (bzr_status s = run_fused<kModeRefract>(ctx, single_lens(mv), job, flags)) return s;
   } else {
     Work w;
-    const uint32_t ch = chunk_for(n);
+    const uint32_t ch = chunk_for(ctx, n);
     if (bzr_status s = ensure_work(ctx, ch, mesh->n, w)) return s;
     Out o{};
     o.rays = d_out;
@@ -2019,7 +2035,7 @@ extern "C" bzr_status bzr_trace_chain(bzr_ctx *ctx, const bzr_mesh *const *lense
     uint32_t nb = 0;
     for (uint32_t l = 0; l < nlens; ++l) nb = std::max(nb, set.lens[l].n);
     Work w;
-    const uint32_t ch = chunk_for(n);
+    const uint32_t ch = chunk_for(ctx, n);
     if (bzr_status s = ensure_work(ctx, ch, nb, w)) return s;
     // the first stage reads the caller's rays and writes every ray's ray / status / segments (no
     // copy or fill launches); later stages update the rays in flight in place, alive = status != NONE
@@ -2277,7 +2293,7 @@ extern "C" bzr_status bzr_illuminate(bzr_ctx *ctx, const bzr_mesh *const *lenses
   const float cell_u = tg->size_u / (float)tg->bins_u, cell_v = tg->size_v / (float)tg->bins_v;
   const size_t cells = (size_t)tg->bins_u * tg->bins_v;
   const bool host = !(flags & BZR_DEVICE_PTRS);
-  const uint32_t B = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(total_rays, 1), kChunk);
+  const uint32_t B = chunk_for(ctx, total_rays);
   if (bzr_status s = ensure_buffer(ctx->scratch, ctx->scratch_bytes,
                                    belt_bytes(em->belts) + round256((size_t)B * 24) + 2 * round256((size_t)B * 4) +
                                        round256(32) + (host ? round256(cells * 4) : 0)))
