@@ -58,7 +58,10 @@ double normd(d3 a) { return std::sqrt(dotd(a, a)); }
 constexpr double kEps = BZR_BVH_EPS_U / 16777216.0;
 constexpr double kPad = BZR_BVH_PAD_U / 16777216.0;
 constexpr double kSlack = 1.0 / (1 << BZR_BVH_KSLACK_LOG2);
-constexpr double kRound1 = 1.0 / (1 << 18);
+#ifndef BZR_BVH_ROUND1_LOG2
+#define BZR_BVH_ROUND1_LOG2 18
+#endif
+constexpr double kRound1 = 1.0 / (1 << BZR_BVH_ROUND1_LOG2);
 
 // Clip convex polygon `poly` (plane points) to { x : g.x + h >= 0 }.
 std::vector<d3> clip(std::vector<d3> const &poly, d3 g, double h) {
