@@ -563,11 +563,15 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
 }
 
 // Candidate search, one 64-ray wave per 64 consecutive rays.
+// BZR_TRAV_XCD (A/B knob): 1 = XCD-contiguous ray ranges (round 1), 0 = dispatch order.
+#ifndef BZR_TRAV_XCD
+#define BZR_TRAV_XCD 1
+#endif
 __global__ __launch_bounds__(kTravBlock) void k_traverse(MeshView m, const float *__restrict__ rays, uint32_t ld,
                                                          uint32_t off, const uint32_t *__restrict__ alive, uint32_t n,
                                                          Work w, uint32_t count_rays) {
   __shared__ uint32_t stack[kTravBlock / 64][kStack];
-  const uint32_t b = xcd_contiguous(blockIdx.x, gridDim.x);
+  const uint32_t b = BZR_TRAV_XCD ? xcd_contiguous(blockIdx.x, gridDim.x) : blockIdx.x;
   traverse_rays(m, rays, ld, off, alive, n, w, count_rays, b * kTravBlock + threadIdx.x, stack[threadIdx.x >> 6]);
 }
 
@@ -1183,13 +1187,30 @@ struct TraceJob {
 #define BZR_TRACE_BLOCK 64
 #endif
 constexpr int kTraceBlock = BZR_TRACE_BLOCK, kTraceWaves = kTraceBlock / 64;
+// Which 64-ray tile block b takes (BZR_TRACE_XCD): 0 = the dispatch order itself (XCD x gets every 8th
+// tile), 1 = xcd_contiguous (each XCD one contiguous range of the image), G > 1 = runs of G tiles dealt
+// round-robin to the XCDs.  0 is the default: a lens covers the middle of the image, so contiguous
+// ranges give the middle XCDs ~2x the work of the outer ones, and a lens's records fit every XCD's L2
+// anyway (cfg4: 6.26 ms with 1, 5.85 with 16, 5.67 with 0; cfg5 fused within 1 %).
+#ifndef BZR_TRACE_XCD
+#define BZR_TRACE_XCD 0
+#endif
+__device__ __forceinline__ uint32_t trace_tile(uint32_t b, uint32_t nblocks) {
+  if (BZR_TRACE_XCD == 0) return b;
+  if (BZR_TRACE_XCD == 1) return xcd_contiguous(b, nblocks);
+  constexpr uint32_t G = BZR_TRACE_XCD;
+  const uint32_t full = nblocks / (kXcds * G) * (kXcds * G);  // whole rounds of 8 runs; the rest stays put
+  if (b >= full) return b;
+  const uint32_t x = b % kXcds, k = b / kXcds;
+  return (k / G * kXcds + x) * G + k % G;
+}
 template <int kMode, bool kFast, bool kCount>
 __global__ __launch_bounds__(kTraceBlock) BZR_TRACE_ATTR void k_trace(LensSet lenses, TraceJob job,
                                                                       unsigned long long *__restrict__ counters) {
   __shared__ TraceLds<kMode> lds[kTraceWaves];
   const uint32_t lane = threadIdx.x & 63u;
   TraceLds<kMode> &L = lds[threadIdx.x >> 6];
-  const uint32_t i = xcd_contiguous(blockIdx.x, gridDim.x) * kTraceBlock + threadIdx.x;
+  const uint32_t i = trace_tile(blockIdx.x, gridDim.x) * kTraceBlock + threadIdx.x;
   const uint32_t n = job.n;
   TraceCtr ctr;
   bool alive = i < n;
