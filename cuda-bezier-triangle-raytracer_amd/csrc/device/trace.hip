@@ -126,6 +126,22 @@ __device__ __forceinline__ uint32_t xcd_contiguous(uint32_t b, uint32_t nblocks)
   const uint32_t q = nblocks / kXcds, r = nblocks % kXcds, x = b % kXcds;
   return x * q + (x < r ? x : r) + b / kXcds;
 }
+// Block b's index under a dealing policy: 0 = dispatch order (XCD x gets every 8th block), 1 =
+// xcd_contiguous, G > 1 = runs of G blocks dealt round-robin to the XCDs (whole rounds of 8 runs; the
+// ragged rest keeps its index).  A bijection on [0, nblocks) in every case.
+template <uint32_t kPolicy>
+__device__ __forceinline__ uint32_t deal_blocks(uint32_t b, uint32_t nblocks) {
+  if constexpr (kPolicy == 0) {
+    return b;
+  } else if constexpr (kPolicy == 1) {
+    return xcd_contiguous(b, nblocks);
+  } else {
+    const uint32_t full = nblocks / (kXcds * kPolicy) * (kXcds * kPolicy);
+    if (b >= full) return b;
+    const uint32_t x = b % kXcds, k = b / kXcds;
+    return (k / kPolicy * kXcds + x) * kPolicy + k % kPolicy;
+  }
+}
 // Threads per k_traverse block: its waves share one CU (scalar cache) and take neighbouring rays.
 #ifndef BZR_TRAV_BLOCK
 #define BZR_TRAV_BLOCK 256
@@ -563,7 +579,8 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
 }
 
 // Candidate search, one 64-ray wave per 64 consecutive rays.
-// BZR_TRAV_XCD (A/B knob): 1 = XCD-contiguous ray ranges (round 1), 0 = dispatch order.
+// BZR_TRAV_XCD (A/B knob, deal_blocks policy): 1 = XCD-contiguous ray ranges (round 1), 0 = dispatch
+// order, G > 1 = runs of G blocks per XCD.
 #ifndef BZR_TRAV_XCD
 #define BZR_TRAV_XCD 1
 #endif
@@ -571,7 +588,7 @@ __global__ __launch_bounds__(kTravBlock) void k_traverse(MeshView m, const float
                                                          uint32_t off, const uint32_t *__restrict__ alive, uint32_t n,
                                                          Work w, uint32_t count_rays) {
   __shared__ uint32_t stack[kTravBlock / 64][kStack];
-  const uint32_t b = BZR_TRAV_XCD ? xcd_contiguous(blockIdx.x, gridDim.x) : blockIdx.x;
+  const uint32_t b = deal_blocks<BZR_TRAV_XCD>(blockIdx.x, gridDim.x);
   traverse_rays(m, rays, ld, off, alive, n, w, count_rays, b * kTravBlock + threadIdx.x, stack[threadIdx.x >> 6]);
 }
 
@@ -1196,13 +1213,7 @@ constexpr int kTraceBlock = BZR_TRACE_BLOCK, kTraceWaves = kTraceBlock / 64;
 #define BZR_TRACE_XCD 0
 #endif
 __device__ __forceinline__ uint32_t trace_tile(uint32_t b, uint32_t nblocks) {
-  if (BZR_TRACE_XCD == 0) return b;
-  if (BZR_TRACE_XCD == 1) return xcd_contiguous(b, nblocks);
-  constexpr uint32_t G = BZR_TRACE_XCD;
-  const uint32_t full = nblocks / (kXcds * G) * (kXcds * G);  // whole rounds of 8 runs; the rest stays put
-  if (b >= full) return b;
-  const uint32_t x = b % kXcds, k = b / kXcds;
-  return (k / G * kXcds + x) * G + k % G;
+  return deal_blocks<BZR_TRACE_XCD>(b, nblocks);
 }
 template <int kMode, bool kFast, bool kCount>
 __global__ __launch_bounds__(kTraceBlock) BZR_TRACE_ATTR void k_trace(LensSet lenses, TraceJob job,
