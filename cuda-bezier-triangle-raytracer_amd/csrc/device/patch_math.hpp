@@ -127,7 +127,46 @@ constexpr uint32_t kFollow2 = 2u, kNone = 3u, kIntersect = 4u;
 namespace exact {
 __device__ __forceinline__ float div_rn(float a, float b) { return a / b; }
 __device__ __forceinline__ float sqrt_rn(float a) { return __builtin_sqrtf(a); }
-__device__ __forceinline__ f3 unit(f3 a, float z) {  // Eigen normalized(): a / sqrt(z), three divisions
+
+// The two sequences above, as LLVM lowers them for gfx950, minus their range handling:
+//   sqrt: v_sqrt_f32, then the neighbours s -/+ 1 ulp are tested with fma residuals; LLVM first scales
+//         z < 2^-96 by 2^32 and passes 0 / inf / NaN through (v_cmp_class);
+//   a/b:  v_div_scale (num, den), v_rcp_f32, one Newton step of the reciprocal, q = num*y, two fma
+//         corrections (the second is v_div_fmas), v_div_fixup (signs, zeros, inf/NaN, overflow).
+// Where v_div_scale scales nothing and v_div_fixup passes the quotient through, the plain fma chain is
+// the same instructions on the same values, so it returns the same correctly rounded bits.  V_DIV_SCALE
+// scales when: num or den is 0; exp(num) - exp(den) >= 96; den is denormal; 1/den or num/den is
+// denormal; |num| < 2^-103.  unit() takes the plain chain only when |a_k| >= 2^-100 for every k and
+// 2^-96 <= z <= 2^40 (so s = sqrt(z) is in [2^-48, 2^20] and |a_k| / s >= 2^-120 is normal; |a_k| <= ~s):
+// none of those cases, no sqrt scaling, no special value.  The three quotients share the divisor, so
+// they share the reciprocal: 1 sqrt + 3 + 3 x 5 instructions instead of 1 + 3 x 11.
+__device__ __forceinline__ float sqrt_unscaled(float z) {
+  const float s = __builtin_amdgcn_sqrtf(z);
+  const float lo = __uint_as_float(__float_as_uint(s) - 1u), hi = __uint_as_float(__float_as_uint(s) + 1u);
+  const float rlo = __builtin_fmaf(-lo, s, z), rhi = __builtin_fmaf(-hi, s, z);
+  const float t = rlo <= 0.0f ? lo : s;
+  return rhi > 0.0f ? hi : t;
+}
+__device__ __forceinline__ float div_unscaled(float a, float b, float y) {  // y: the refined 1/b
+  float q = a * y;
+  float r = __builtin_fmaf(-b, q, a);
+  q = __builtin_fmaf(r, y, q);
+  r = __builtin_fmaf(-b, q, a);
+  return __builtin_fmaf(r, y, q);
+}
+#ifndef BZR_UNIT_SHARED
+#define BZR_UNIT_SHARED 1
+#endif
+__device__ __forceinline__ f3 unit(f3 a, float z) {  // Eigen normalized() for z > 0: a / sqrt(z), three divisions
+#if BZR_UNIT_SHARED
+  const float m = fminf(fminf(fabsf(a.x), fabsf(a.y)), fabsf(a.z));
+  if (m >= 0x1p-100f && z >= 0x1p-96f && z <= 0x1p40f) {
+    const float s = sqrt_unscaled(z);
+    const float y0 = __builtin_amdgcn_rcpf(s);
+    const float y = __builtin_fmaf(__builtin_fmaf(-s, y0, 1.0f), y0, y0);
+    return mk(div_unscaled(a.x, s, y), div_unscaled(a.y, s, y), div_unscaled(a.z, s, y));
+  }
+#endif
   float s = sqrt_rn(z);
   return mk(div_rn(a.x, s), div_rn(a.y, s), div_rn(a.z, s));
 }

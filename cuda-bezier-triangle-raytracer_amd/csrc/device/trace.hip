@@ -2100,6 +2100,39 @@ extern "C" bzr_status bzr_trace_chain(bzr_ctx *ctx, const bzr_mesh *const *lense
   return BZR_OK;
 }
 
+// ------------------------------------------------------------ test hook: normalized()
+namespace {
+// Row k of out (k < 3): the product's exact normalized() (patch_math.hpp unit, shared-reciprocal chain
+// where its guard allows); rows 3..5: sqrt_rn / div_rn per component (the compiler's own lowering).
+__global__ __launch_bounds__(kBlock) void k_debug_unit(const float *__restrict__ a, uint32_t n,
+                                                       float *__restrict__ out) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const f3 v = mk(a[i], a[(size_t)n + i], a[(size_t)2 * n + i]);
+  const f3 u = normalized(v);
+  const float z = dot(v, v);
+  f3 w = v;
+  if (z > 0.0f) {
+    const float s = sqrt_rn(z);
+    w = mk(div_rn(v.x, s), div_rn(v.y, s), div_rn(v.z, s));
+  }
+  const float r[6] = {u.x, u.y, u.z, w.x, w.y, w.z};
+#pragma unroll
+  for (int k = 0; k < 6; ++k) out[(size_t)k * n + i] = r[k];
+}
+}  // namespace
+
+extern "C" bzr_status bzr_debug_unit(void *ctxp, const float *a, uint32_t n, float *out) {
+  bzr_ctx *ctx = static_cast<bzr_ctx *>(ctxp);
+  if (!ctx) return set_error(BZR_ERR_INVALID_ARGUMENT, "null context");
+  if (n == 0) return BZR_OK;
+  if (!a || !out) return set_error(BZR_ERR_INVALID_ARGUMENT, "null buffer");
+  DeviceGuard g(ctx->device);
+  hipLaunchKernelGGL(k_debug_unit, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, ctx->stream, a, n, out);
+  BZR_HIP(hipGetLastError());
+  return BZR_OK;
+}
+
 // ------------------------------------------------------------ tessellation
 extern "C" uint32_t bzr_internal_unit_subtriangles(int32_t divisor, float *out);  // host (patch_build.cpp)
 

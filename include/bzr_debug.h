@@ -28,6 +28,11 @@ int32_t bzr_debug_bounding_sphere(const void *patches, uint32_t n, uint32_t stri
  * [3] waves.  Returns 0 on success. */
 int32_t bzr_debug_traverse(const void *patches, uint32_t n, uint32_t stride, const float *rays, uint32_t nr,
                            uint8_t *hits, uint64_t stats[4]);
+/* Device check of the exact normalized() (Eigen a / sqrt(a.a)): `a` is device memory [3][n], `out` device
+ * memory [6][n]: rows 0-2 the product's normalized(a), rows 3-5 the same with the compiler's correctly
+ * rounded sqrt and one division per component.  Asynchronous on the context's stream.  ctx is a
+ * bzr_ctx* (bzr.h). */
+int32_t bzr_debug_unit(void *ctx, const float *a, uint32_t n, float *out);
 #ifdef __cplusplus
 }
 #endif
