@@ -495,19 +495,19 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
   const float4 *leaf = near_tier ? m.leaf_near : m.leaf;
   const f3 inv = mk(safe_inv(d.x), safe_inv(d.y), safe_inv(d.z));
   const f3 sinv = mk(s.x * inv.x, s.y * inv.y, s.z * inv.z);
-  int sp = 0;
-  if (m.n > 0 && __any(active)) {
-    stk[0] = 0u;
-    sp = 1;
-  }
-  while (sp > 0) {
-    const uint32_t node = __builtin_amdgcn_readfirstlane(stk[--sp]);
+  int sp = 0;  // the node to visit next stays in a scalar register; the other hit children go to stk
+  uint32_t next = (m.n > 0 && __any(active)) ? 0u : 0xFFFFFFFFu;
+  unsigned long long next_hm = 0ull;
+  while (next != 0xFFFFFFFFu || sp > 0) {
+    const uint32_t node = next != 0xFFFFFFFFu ? next : __builtin_amdgcn_readfirstlane(stk[--sp]);
+    next = 0xFFFFFFFFu;
     bool hit[4];
     uint32_t ch[4];
     node_children(nodes, obb, node, active, s, d, sinv, inv, hit, ch);
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      if (!__any(hit[c])) continue;
+      const unsigned long long hm = __ballot(hit[c]);
+      if (hm == 0ull) continue;
       if (ch[c] & bzr_host::kLeafFlag) {
         const u32x16 r = *((const cu32x16 *)(uintptr_t)leaf + (ch[c] & ~bzr_host::kLeafFlag));
         const float4 q0 = make_float4(__uint_as_float(r[0]), __uint_as_float(r[1]), __uint_as_float(r[2]), __uint_as_float(r[3]));
@@ -518,10 +518,13 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
           if (cnt < kMaxCand) w.cand[(size_t)cnt * n + i] = r[15];
           cnt = cnt < kMaxCand ? cnt + 1 : kOverflow;
         }
-      } else if (sp < kStack) {
-        stk[sp++] = ch[c];
-      } else {  // traversal stack exhausted: resolve these rays with the full scan
-        if (hit[c]) cnt = kOverflow;
+      } else {
+        if (next != 0xFFFFFFFFu) {
+          if (sp < kStack) stk[sp++] = next;
+          else if ((next_hm >> (threadIdx.x & 63u)) & 1ull) cnt = kOverflow;  // stack exhausted: full scan
+        }
+        next = ch[c];
+        next_hm = hm;
       }
     }
   }
@@ -1033,18 +1036,19 @@ __device__ __forceinline__ void trace_segment(const MeshView &m, f3 s, f3 d, boo
   const float4 *leaf = near_tier ? m.leaf_near : m.leaf;
   const f3 inv = mk(safe_inv(d.x), safe_inv(d.y), safe_inv(d.z));
   const f3 sinv = mk(s.x * inv.x, s.y * inv.y, s.z * inv.z);
+  // The node to visit next is held in a scalar register (`next`); only the other hit children go to the
+  // LDS stack, so a descent costs no LDS round trip (same visit order as pushing them all).
   int sp = 0;
-  if (m.n > 0 && __any(act)) {
-    L.stack[0] = 0u;
-    sp = 1;
-  }
+  uint32_t next = (m.n > 0 && __any(act)) ? 0u : kNo;
+  unsigned long long next_hm = 0ull;  // the lanes whose rays hit `next`'s box
   uint32_t scan = kNo;                // next patch of the full scan (kNo: not scanning)
   uint32_t join = kNo, join_src = 0;  // a retry waiting for a later leaf's pass: that leaf, scanned patch
   uint32_t parked_nb = kNo;           // the patch whose cNone result is parked for this lane
   for (;;) {
     uint32_t ne = 0;  // collected leaves (uniform)
-    while (sp > 0 && ne + 4u <= kEntries) {
-      const uint32_t node = __builtin_amdgcn_readfirstlane(L.stack[--sp]);
+    while ((next != kNo || sp > 0) && ne + 4u <= kEntries) {
+      const uint32_t node = next != kNo ? next : __builtin_amdgcn_readfirstlane(L.stack[--sp]);
+      next = kNo;
       if (kCount) ++ctr.nodes;
       bool hit[4];
       uint32_t ch[4];
@@ -1072,10 +1076,13 @@ __device__ __forceinline__ void trace_segment(const MeshView &m, f3 s, f3 d, boo
             }
             ++ne;
           }
-        } else if (sp < kStack) {
-          L.stack[sp++] = ch[c];
-        } else {  // traversal stack exhausted: these lanes take the full scan
-          if (hit[c]) ovf = true;
+        } else {
+          if (next != kNo) {
+            if (sp < kStack) L.stack[sp++] = next;
+            else if (lane_bit(next_hm, lane)) ovf = true;  // traversal stack exhausted: these lanes take the full scan
+          }
+          next = ch[c];
+          next_hm = hm;
         }
       }
     }
