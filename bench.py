@@ -226,15 +226,11 @@ def main():
     pending = [None, None]
     frames = [0]
 
-    def step(ev=None):
-        if ev is not None:
-            ev[0].record(stream)
+    def step():
         if chain:
             bzr_amd.trace_chain(ctx, meshes, ris, rays, out_rays, out_status, out_seg, mode=mode)
         else:
             bzr_amd.intersect(ctx, meshes[0], rays, hits, mode=mode)
-        if ev is not None:
-            ev[1].record(stream)
         if gather:
             slot = frames[0] % 2
             if pending[slot] is not None:
@@ -271,19 +267,23 @@ def main():
         dist.all_reduce(seg_total)
     seg_total = int(seg_total.item())
 
-    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    # one HIP event pair around the K steps (a timing event between two frames costs the next frame
+    # ~0.15 ms on cfg4: per-step events inside the timed region slowed the measured work by ~3 %)
+    events = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
+    events[0].record(stream)
     for k in range(a.steps):
-        step(events[k])
+        step()
+    events[1].record(stream)
     drain()  # the last frames' gathers complete inside the timed region
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
-    chain_ms = float(np.mean([s.elapsed_time(e) for s, e in events]))
+    chain_ms = events[0].elapsed_time(events[1]) / a.steps
     # per-kernel HIP-event timing on the kernels' stream, in a separate untimed pass of the same
     # K steps (the per-launch events would otherwise sit inside the timed region)
     ctx.timing(True)

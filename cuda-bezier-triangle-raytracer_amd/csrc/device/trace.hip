@@ -903,6 +903,12 @@ constexpr uint32_t kCounterReplicas = 64;
 struct TraceCtr {  // wave-uniform work counters (kCount)
   uint32_t nodes = 0, leaves = 0, gate_tests = 0, rounds = 0, pairs = 0, follows = 0, segments = 0, ovf = 0;
 };
+// BZR_TRACE_PRIO (default 3; 0 = off): wave priority (s_setprio) of k_trace's BVH walk phase, back to 0
+// for the Newton passes.  The walk is a chain of dependent scalar loads with little VALU work; issuing
+// it ahead of the VALU-bound passes of the CU's other waves keeps its loads in flight (cfg4 -3 %).
+#ifndef BZR_TRACE_PRIO
+#define BZR_TRACE_PRIO 3
+#endif
 #ifndef BZR_TRACE_ENTRIES
 #define BZR_TRACE_ENTRIES 16
 #endif
@@ -1046,6 +1052,9 @@ __device__ __forceinline__ void trace_segment(const MeshView &m, f3 s, f3 d, boo
   uint32_t parked_nb = kNo;           // the patch whose cNone result is parked for this lane
   for (;;) {
     uint32_t ne = 0;  // collected leaves (uniform)
+#if BZR_TRACE_PRIO
+    __builtin_amdgcn_s_setprio(BZR_TRACE_PRIO);  // the walk is latency-bound: issue it ahead of Newton passes
+#endif
     while ((next != kNo || sp > 0) && ne + 4u <= kEntries) {
       const uint32_t node = next != kNo ? next : __builtin_amdgcn_readfirstlane(L.stack[--sp]);
       next = kNo;
@@ -1108,6 +1117,9 @@ __device__ __forceinline__ void trace_segment(const MeshView &m, f3 s, f3 d, boo
       ++scan;
     }
     // the collected leaves' passes, in order
+#if BZR_TRACE_PRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
     for (uint32_t e = 0; e < ne; ++e) {
       const uint32_t b = __builtin_amdgcn_readfirstlane(L.eid[e]);
       const auto hp = uniform_patch(m.full, b);
