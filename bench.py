@@ -250,10 +250,6 @@ def main():
                 pending[k].wait()
                 pending[k] = None
 
-    for _ in range(a.warmup):
-        step()
-    drain()
-    torch.cuda.synchronize()
     # work counters of one frame (device-side; measured here, outside the timed region)
     ctx.counters(True)
     ctx.counters_report()
@@ -266,9 +262,12 @@ def main():
     if world > 1:
         dist.all_reduce(seg_total)
     seg_total = int(seg_total.item())
+    # the W warmup steps run right before the timed ones (no host round trip in between)
+    for _ in range(a.warmup):
+        step()
+    drain()
 
-    # one HIP event pair around the K steps (a timing event between two frames costs the next frame
-    # ~0.15 ms on cfg4: per-step events inside the timed region slowed the measured work by ~3 %)
+    # one HIP event pair around the K steps (no timing markers between the frames)
     events = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
     if world > 1:
         dist.barrier()
