@@ -16,6 +16,8 @@ weak: the image grows to side x (side*N).  Each frame's results are gathered to 
 the timed region, double-buffered so frame k's gather overlaps frame k+1's tracing: --gather image
 (default) the per-primary status + segment-count word (4 B; the final rays stay in each rank's HBM),
 --gather rays the final rays too (28 B per primary), --gather none nothing (tracing alone).
+--inflight F (default 2): frame k runs on slot k % F (its own context, stream and output buffers), so
+the next frame's waves fill the GPU while a frame's slowest waves finish; every frame is traced in full.
 
 Prints ONE JSON line on rank 0; fields are described in DESIGN.md (d).
 """
@@ -58,6 +60,8 @@ def parse():
     p.add_argument("--pipeline", default="fused", choices=["fused", "staged", "auto"],
                    help="culled-path pipeline (include/bzr.h BZR_PIPELINE_*; same output bits): fused = one k_trace "
                         "kernel per frame (default), staged = the multi-kernel path, auto = the library's choice")
+    p.add_argument("--inflight", type=int, default=2,
+                   help="frames in flight (each on its own context, stream and output buffers)")
     p.add_argument("--mode", default="parity", choices=["parity", "fast"],
                    help="fast = BZR_MODE_FAST Newton stage (contracted FMA, approximate div/sqrt; not bit-exact)")
     p.add_argument("--cpu-baseline", default="on", choices=["on", "off"])
@@ -194,7 +198,10 @@ def main():
     t0 = time.perf_counter()
     meshes = [bzr_amd.DeviceMesh(ctx, p) for p in patches]  # upload + BVH build
     upload_s = time.perf_counter() - t0
-    stream = torch.cuda.Stream(dev)   # one stream for the kernels, torch ops and the timing events
+    # one stream per frame slot (--inflight), created back to back: torch hands out its pooled streams
+    # round-robin, and consecutive ones sit on different hardware queues, so the slots' frames overlap
+    streams = [torch.cuda.Stream(dev) for _ in range(max(1, a.inflight))]
+    stream = streams[0]  # slot 0: the kernels, torch ops and the timing events
     torch.cuda.set_stream(stream)
     ctx.use_torch_stream(stream)
     mode = bzr_amd.ACCEL_NONE if a.accel == "none" else bzr_amd.MODE_PARITY
@@ -206,12 +213,20 @@ def main():
     _, _, rays_np = frame.rank_rays(cfg, rank, world, side, height)
     n = rays_np.shape[1]
     rays = torch.from_numpy(rays_np).to(dev)
+    # Frames in flight: frame k runs on slot k % F -- its own context, stream and output buffers -- so the
+    # next frame's waves fill the GPU while this frame's slowest waves finish (a frame's last waves run
+    # up to ~6x the median wave; with one frame in flight their tail idles most of the chip).
+    F = max(1, a.inflight)
+    ctxs = [ctx] + [bzr_amd.Context(local) for _ in range(F - 1)]
+    for c, st in zip(ctxs[1:], streams[1:]):
+        c.use_torch_stream(st)
     if chain:
-        out_rays = torch.empty((6, n), dtype=torch.float32, device=dev)
-        out_status = torch.empty(n, dtype=torch.int32, device=dev)
-        out_seg = torch.empty(n, dtype=torch.int32, device=dev)
+        outs = [(torch.empty((6, n), dtype=torch.float32, device=dev), torch.empty(n, dtype=torch.int32, device=dev),
+                 torch.empty(n, dtype=torch.int32, device=dev)) for _ in range(F)]
+        out_rays, out_status, out_seg = outs[0]
     else:
-        hits = torch.empty((13, n), dtype=torch.float32, device=dev)
+        outs = [torch.empty((13, n), dtype=torch.float32, device=dev) for _ in range(F)]
+        hits = outs[0]
     gather = world > 1 and a.gather != "none"
     # rays layout: the whole result (chain: 6 ray rows + status/segment word; intersect: the 13 hit rows);
     # image layout: one word per primary (chain: status | segments << 8; intersect: the hit's `what` row)
@@ -226,23 +241,31 @@ def main():
     pending = [None, None]
     frames = [0]
 
-    def step():
-        if chain:
-            bzr_amd.trace_chain(ctx, meshes, ris, rays, out_rays, out_status, out_seg, mode=mode)
-        else:
-            bzr_amd.intersect(ctx, meshes[0], rays, hits, mode=mode)
-        if gather:
-            slot = frames[0] % 2
-            if pending[slot] is not None:
-                pending[slot].wait()
+    def step(inflight=F):
+        f = frames[0] % inflight  # frame slot: context, stream, outputs
+        with torch.cuda.stream(streams[f]):
             if chain:
-                frame.pack(out_rays, out_status, out_seg, packed[slot])
-            elif rows == 1:
-                packed[slot][0, :n].copy_(hits[11])
+                bzr_amd.trace_chain(ctxs[f], meshes, ris, rays, *outs[f], mode=mode)
             else:
-                packed[slot][:, :n].copy_(hits)
-            pending[slot] = frame.gather(packed[slot], world, rank, gather_list=gather_lists[slot], async_op=True)
+                bzr_amd.intersect(ctxs[f], meshes[0], rays, outs[f], mode=mode)
+            if gather:
+                slot = frames[0] % 2
+                if pending[slot] is not None:
+                    pending[slot].wait()
+                if chain:
+                    frame.pack(*outs[f], packed[slot])
+                elif rows == 1:
+                    packed[slot][0, :n].copy_(outs[f][11])
+                else:
+                    packed[slot][:, :n].copy_(outs[f])
+                pending[slot] = frame.gather(packed[slot], world, rank, gather_list=gather_lists[slot], async_op=True)
         frames[0] += 1
+
+    def join_streams():  # stream 0 waits for the other slots' queued frames
+        for st in streams[1:]:
+            ev = torch.cuda.Event()
+            ev.record(st)
+            streams[0].wait_event(ev)
 
     def drain():
         for k in range(2):
@@ -253,7 +276,8 @@ def main():
     # work counters of one frame (device-side; measured here, outside the timed region)
     ctx.counters(True)
     ctx.counters_report()
-    step()
+    frames[0] = 0
+    step(inflight=1)
     drain()
     work_cnt = ctx.counters_report()
     ctx.counters(False)
@@ -274,8 +298,11 @@ def main():
     torch.cuda.synchronize()
     t_start = time.perf_counter()
     events[0].record(stream)
+    for st in streams[1:]:
+        st.wait_event(events[0])
     for k in range(a.steps):
         step()
+    join_streams()
     events[1].record(stream)
     drain()  # the last frames' gathers complete inside the timed region
     torch.cuda.synchronize()
@@ -288,7 +315,7 @@ def main():
     ctx.timing(True)
     ctx.timing_report()  # reset
     for k in range(a.steps):
-        step()
+        step(inflight=1)  # slot 0's context only: kernel durations without a neighbouring frame
     drain()
     kernels = ctx.timing_report()
     ctx.timing(False)
@@ -360,6 +387,7 @@ def main():
                                + (f", RCCL gather of every frame to rank 0 (overlapped with the next frame): "
                                   f"{rows * 4} B per primary ({a.gather})" if gather else ""),
                 "pipeline": a.pipeline,
+                "frames_in_flight": F,
                 "scan": "BVH-culled (bit-identical to brute force)" if a.accel == "bvh" else "brute force",
                 "numerics": "parity: bit-identical to the CPU oracle" if a.mode == "parity" else
                             "fast: exact planar gate, Newton stage with FMA + approximate div/sqrt (SURVEY 8c fast gates)",

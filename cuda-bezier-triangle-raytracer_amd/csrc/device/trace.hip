@@ -100,6 +100,8 @@ struct bzr_ctx {
   uint32_t chunk_cap = 0;                // staged-path rays per chunk (0: not yet sized, chunk_for)
   bool counting = false;                 // work counters (bzr_ctx_counters)
   unsigned long long *counters = nullptr;  // device [BZR_COUNTER_COUNT]
+  unsigned long long *wave_clock = nullptr;  // test hook (bzr_debug_wave_clock): per k_trace wave, device
+  uint32_t wave_clock_cap = 0;
 };
 
 namespace {
@@ -1206,6 +1208,7 @@ struct TraceJob {
   uint32_t expected_all;
   uint32_t n;
   uint32_t ld;               // row stride of rays / out_rays / hits (>= n)
+  unsigned long long *wave_clock;  // optional test hook: [2 * waves] start, duration (s_memtime ticks)
 };
 
 // BZR_TRACE_WPE (A/B knob, default 0 = the compiler's choice): amdgpu_waves_per_eu lower bound for k_trace.
@@ -1241,6 +1244,7 @@ __global__ __launch_bounds__(kTraceBlock) BZR_TRACE_ATTR void k_trace(LensSet le
   const uint32_t lane = threadIdx.x & 63u;
   TraceLds<kMode> &L = lds[threadIdx.x >> 6];
   const uint32_t i = trace_tile(blockIdx.x, gridDim.x) * kTraceBlock + threadIdx.x;
+  const unsigned long long t_start = job.wave_clock ? __builtin_amdgcn_s_memtime() : 0ull;
   const uint32_t n = job.n;
   TraceCtr ctr;
   bool alive = i < n;
@@ -1281,6 +1285,11 @@ __global__ __launch_bounds__(kTraceBlock) BZR_TRACE_ATTR void k_trace(LensSet le
     store_ray(job.out_rays, job.ld, i, s, d);
     job.status[i] = st;
     if (kMode == kModeStage && job.segments) job.segments[i] = seg;
+  }
+  if (job.wave_clock && lane == 0u) {  // the wave's tile (ray index / 64): start tick and duration
+    const unsigned long long t_end = __builtin_amdgcn_s_memtime();
+    job.wave_clock[2 * (i >> 6)] = t_start;
+    job.wave_clock[2 * (i >> 6) + 1] = t_end - t_start;
   }
   if (kCount && lane < 8u) {  // one atomic per counter per wave, spread over kCounterReplicas copies
     const uint32_t v[8] = {ctr.segments, ctr.pairs, ctr.follows, ctr.ovf, ctr.nodes, ctr.leaves, ctr.gate_tests,
@@ -1621,7 +1630,9 @@ bzr_status run_fused(bzr_ctx *ctx, const LensSet &set, const TraceJob &job, uint
   if (job.n == 0) return BZR_OK;
   const bool fast = use_fast(flags), count = ctx->counting && ctx->counters;
   const dim3 grid((job.n + kTraceBlock - 1) / kTraceBlock), block(kTraceBlock);
-  auto go = [&](auto kernel) { launch_on(ctx, ctx->stream, block, BZR_KERNEL_TRACE, kernel, grid, set, job, ctx->counters); };
+  TraceJob j = job;
+  j.wave_clock = (ctx->wave_clock && ctx->wave_clock_cap >= (job.n + 63) / 64) ? ctx->wave_clock : nullptr;
+  auto go = [&](auto kernel) { launch_on(ctx, ctx->stream, block, BZR_KERNEL_TRACE, kernel, grid, set, j, ctx->counters); };
   if (fast) {
     if (count) go(k_trace<kMode, true, true>);
     else go(k_trace<kMode, true, false>);
@@ -2140,6 +2151,14 @@ __global__ __launch_bounds__(kBlock) void k_debug_unit(const float *__restrict__
   for (int k = 0; k < 6; ++k) out[(size_t)k * n + i] = r[k];
 }
 }  // namespace
+
+extern "C" bzr_status bzr_debug_wave_clock(void *ctxp, unsigned long long *clock, uint32_t waves) {
+  bzr_ctx *ctx = static_cast<bzr_ctx *>(ctxp);
+  if (!ctx) return set_error(BZR_ERR_INVALID_ARGUMENT, "null context");
+  ctx->wave_clock = clock;
+  ctx->wave_clock_cap = clock ? waves : 0u;
+  return BZR_OK;
+}
 
 extern "C" bzr_status bzr_debug_unit(void *ctxp, const float *a, uint32_t n, float *out) {
   bzr_ctx *ctx = static_cast<bzr_ctx *>(ctxp);

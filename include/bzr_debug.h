@@ -33,6 +33,11 @@ int32_t bzr_debug_traverse(const void *patches, uint32_t n, uint32_t stride, con
  * rounded sqrt and one division per component.  Asynchronous on the context's stream.  ctx is a
  * bzr_ctx* (bzr.h). */
 int32_t bzr_debug_unit(void *ctx, const float *a, uint32_t n, float *out);
+/* Per-wave timing of the fused kernel: while set, every fused call (k_trace, one 64-ray wave per 64
+ * consecutive rays) of `n` <= 64 * waves rays writes clock[2w] = the wave's start (s_memtime ticks) and
+ * clock[2w+1] = its duration, for wave w = ray index / 64.  `clock` is device memory; NULL turns it off.
+ * ctx is a bzr_ctx* (bzr.h). */
+int32_t bzr_debug_wave_clock(void *ctx, unsigned long long *clock, uint32_t waves);
 #ifdef __cplusplus
 }
 #endif
