@@ -154,6 +154,10 @@ constexpr int kTravBlock = BZR_TRAV_BLOCK;
 #define BZR_SLAB_FMA 1
 #endif
 // BZR_NEWTON_XCD (default 0): k_newton waves take chunks in XCD-contiguous order (measured +6 %, off).
+// BZR_GATE_FLAT (default 1): planar_gate without early-out branches (see there).
+#ifndef BZR_GATE_FLAT
+#define BZR_GATE_FLAT 1
+#endif
 #ifndef BZR_NEWTON_XCD
 #define BZR_NEWTON_XCD 0
 #endif
@@ -218,6 +222,20 @@ __device__ __forceinline__ Hit no_hit() {
 // Planar gate of BezierTriangle::intersect with cThis (reference/bezierTriangle.cpp:124-131),
 // evaluated from the 64-byte scan record; same arithmetic as patch_intersect's first lines.
 __device__ __forceinline__ bool planar_gate(float4 q0, float4 q1, float4 q2, float4 q3, f3 s, f3 d) {
+#if BZR_GATE_FLAT
+  // Branch-free: every term is evaluated and the conditions are combined with '&' (the same decision as
+  // plane_ray's early outs below -- a lane with |cos| < 1e-5 fails whatever its t), so the walk runs no
+  // exec-mask bookkeeping (s_and_saveexec / s_or exec per condition) on the scalar unit.
+  const f3 n = mk(q0.x, q0.y, q0.z);
+  const float cs = dot(d, n);
+  const float t = div_rn(q0.w - dot(n, s), cs);
+  const f3 ip = add(s, scale(d, t));
+  const bool valid = (fabsf(cs) >= 0.00001f) & (t > 0.0f) & (fabsf(t) > -q1.x) & (fabsf(t) > q1.y);
+  const float b0 = q1.z * ip.x + (q1.w * ip.y + q2.x * ip.z);
+  const float b1 = q2.y * ip.x + (q2.z * ip.y + q2.w * ip.z);
+  const float b2 = q3.x * ip.x + (q3.y * ip.y + q3.z * ip.z);
+  return valid & (b0 >= 0.0f) & (b0 <= 1.0f) & (b1 >= 0.0f) & (b1 <= 1.0f) & (b2 >= 0.0f) & (b2 <= 1.0f);
+#else
   f3 n = mk(q0.x, q0.y, q0.z);
   f3 ip;
   float ic, it;
@@ -228,6 +246,7 @@ __device__ __forceinline__ bool planar_gate(float4 q0, float4 q1, float4 q2, flo
   float b1 = q2.y * ip.x + (q2.z * ip.y + q2.w * ip.z);
   float b2 = q3.x * ip.x + (q3.y * ip.y + q3.z * ip.z);
   return b0 >= 0.0f && b0 <= 1.0f && b1 >= 0.0f && b1 <= 1.0f && b2 >= 0.0f && b2 <= 1.0f;
+#endif
 }
 
 // One iteration of the reference loop body: patch b with cThis, and on a follow-side result its
@@ -516,7 +535,7 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
         const float4 q1 = make_float4(__uint_as_float(r[4]), __uint_as_float(r[5]), __uint_as_float(r[6]), __uint_as_float(r[7]));
         const float4 q2 = make_float4(__uint_as_float(r[8]), __uint_as_float(r[9]), __uint_as_float(r[10]), __uint_as_float(r[11]));
         const float4 q3 = make_float4(__uint_as_float(r[12]), __uint_as_float(r[13]), __uint_as_float(r[14]), 0.0f);
-        if (hit[c] && planar_gate(q0, q1, q2, q3, s, d)) {
+        if (hit[c] & planar_gate(q0, q1, q2, q3, s, d)) {
           if (cnt < kMaxCand) w.cand[(size_t)cnt * n + i] = r[15];
           cnt = cnt < kMaxCand ? cnt + 1 : kOverflow;
         }
@@ -1074,7 +1093,7 @@ __device__ __forceinline__ void trace_segment(const MeshView &m, f3 s, f3 d, boo
           const float4 g1 = make_float4(__uint_as_float(r[4]), __uint_as_float(r[5]), __uint_as_float(r[6]), __uint_as_float(r[7]));
           const float4 g2 = make_float4(__uint_as_float(r[8]), __uint_as_float(r[9]), __uint_as_float(r[10]), __uint_as_float(r[11]));
           const float4 g3 = make_float4(__uint_as_float(r[12]), __uint_as_float(r[13]), __uint_as_float(r[14]), 0.0f);
-          const bool pass = hit[c] && planar_gate(g0, g1, g2, g3, s, d);
+          const bool pass = hit[c] & planar_gate(g0, g1, g2, g3, s, d);
           if (kCount) {
             ++ctr.leaves;
             ctr.gate_tests += popc64(hm);
