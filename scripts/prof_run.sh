@@ -5,7 +5,9 @@
 # The rocprofv3 databases are summarised on the box (scripts/prof_summary.py -> $TAG/summary.txt and
 # $TAG/pmc_traffic.json) and then deleted, so the pulled gpurun_out/ stays small.
 R="$GRAFT_REPO_ROOT"; OUT="$R/gpurun_out/${TAG:-prof}"; mkdir -p "$OUT"; cd /tmp && export TMPDIR=/tmp
-B="$R/bench.py --steps ${STEPS:-5} --warmup 1 --cpu-baseline off ${BENCH:-}"
+# --inflight 1: each launch runs alone, so the trace's per-launch durations compare with bench.py's
+# roofline.avg_launch_ms (measured on serialized launches); with two frames in flight the launches overlap.
+B="$R/bench.py --steps ${STEPS:-5} --warmup 1 --cpu-baseline off --inflight 1 ${BENCH:-}"
 run() {  # run <name> <rocprof args...>
   local name=$1; shift
   timeout -k 10 300 rocprofv3 "$@" -d "$OUT/$name" -o run -- python3 $B > "$OUT/$name.log" 2>&1
