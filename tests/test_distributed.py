@@ -81,3 +81,22 @@ def test_image_layout_gather(bzr, orc, tmp_path, world, side):
     flat = rows * width + cols
     assert np.array_equal(got["status"][flat], s) and np.array_equal(got["seg"][flat], g)
     assert (got["status"] != 0).any()
+
+
+@pytest.mark.parametrize("world", [1, 3, 8])
+def test_tile_deal_covers_the_image_centre_first(world):
+    """configs.shard_pixels: the ranks' tiles partition the image (every pixel once), each rank's 64x64
+    tiles listed nearest the image centre first, each tile in 8x8 wavefront blocks."""
+    from bzr_amd.configs import shard_pixels
+
+    cfg, side = CONFIGS["cfg4"], 512
+    seen = np.zeros(side * side, np.int64)
+    for r in range(world):
+        rows, cols = shard_pixels(cfg, r, world, side=side)
+        seen[rows * side + cols] += 1
+        tr, tc = rows.reshape(-1, 4096).mean(axis=1) + 0.5, cols.reshape(-1, 4096).mean(axis=1) + 0.5  # tile centres
+        dist2 = (tr - side / 2) ** 2 + (tc - side / 2) ** 2
+        assert np.all(np.diff(dist2) >= -1e-9)
+        w = rows.reshape(-1, 64)  # one wavefront: an 8x8 block
+        assert np.all(w.max(axis=1) - w.min(axis=1) == 7)
+    assert np.all(seen == 1)

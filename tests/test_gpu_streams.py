@@ -63,3 +63,58 @@ def test_stream_switch_orders_after_previous_stream(bzr):
     sb.synchronize()
     ctx.use_own_stream()
     assert np.array_equal(hits.cpu().numpy().view(np.uint32), want.view(np.uint32))
+
+
+def test_frames_in_flight_on_two_contexts_match_one_stream(bzr):
+    """bench.py's frames in flight: two contexts on one device share the lens meshes, each launching on
+    its own stream into its own outputs, frames alternating -- every frame's bits equal a lone call's."""
+    torch = pytest.importorskip("torch")
+    cfg = CONFIGS["cfg4"]
+    lenses = [build_lens(bzr.TriMesh, l).bezier_patches() for l in cfg.lenses]
+    ris = [l.ri for l in cfg.lenses]
+    c0, c1 = bzr.Context(0), bzr.Context(0)
+    meshes = [bzr.DeviceMesh(c0, p) for p in lenses]  # device-scoped: usable from c1 too
+    rays = torch.from_numpy(grid_rays(cfg, side=512)).cuda()
+    n = rays.shape[1]
+    want = bzr.trace_chain(c0, meshes, ris, rays.cpu().numpy())
+    s0, s1 = torch.cuda.Stream(), torch.cuda.Stream()
+    c0.use_torch_stream(s0)
+    c1.use_torch_stream(s1)
+    outs = [(torch.empty((6, n), device="cuda"), torch.empty(n, dtype=torch.int32, device="cuda"),
+             torch.empty(n, dtype=torch.int32, device="cuda")) for _ in range(2)]
+    for k in range(6):
+        ctx, st = (c0, s0) if k % 2 == 0 else (c1, s1)
+        with torch.cuda.stream(st):
+            bzr.trace_chain(ctx, meshes, ris, rays, *outs[k % 2])
+    torch.cuda.synchronize()
+    for o, s, g in outs:
+        assert np.array_equal(o.cpu().numpy().view(np.uint32), want[0].view(np.uint32))
+        assert np.array_equal(s.cpu().numpy().astype(np.uint32), want[1])
+        assert np.array_equal(g.cpu().numpy().astype(np.uint32), want[2])
+
+
+def test_wave_clock_hook_times_every_wave(bzr):
+    """bzr_debug_wave_clock (include/bzr_debug.h): one start / duration pair per 64-ray wave of a fused
+    call, durations positive; turning it off leaves the buffer alone."""
+    import ctypes
+
+    torch = pytest.importorskip("torch")
+    cfg = CONFIGS["cfg2"]
+    lens = build_lens(bzr.TriMesh, cfg.lenses[0]).bezier_patches()
+    ctx = bzr.Context(0)
+    ctx.use_torch_stream()
+    dm = bzr.DeviceMesh(ctx, lens)
+    rays = torch.from_numpy(grid_rays(cfg, side=256)).cuda()
+    waves = rays.shape[1] // 64
+    clock = torch.zeros(2 * waves, dtype=torch.int64, device="cuda")
+    L = bzr.lib()
+    assert L.bzr_debug_wave_clock(ctx.handle, ctypes.c_void_p(clock.data_ptr()), waves) == 0
+    bzr.trace_chain(ctx, [dm], [1.3], rays, mode=bzr.MODE_PARITY | bzr.PIPELINE_FUSED)
+    torch.cuda.synchronize()
+    assert L.bzr_debug_wave_clock(ctx.handle, None, 0) == 0
+    c = clock.view(-1, 2).cpu().numpy()
+    assert (c[:, 1] > 0).all() and (c[:, 0] > 0).all()
+    clock.zero_()
+    bzr.trace_chain(ctx, [dm], [1.3], rays, mode=bzr.MODE_PARITY | bzr.PIPELINE_FUSED)
+    torch.cuda.synchronize()
+    assert int(clock.abs().sum()) == 0
