@@ -126,3 +126,30 @@ def test_empty_and_ragged_batches(bzr, orc, ctx, cfg2_lens):
     fo, fs, fg = bzr.trace_chain(ctx, [dm], [1.3], np.ascontiguousarray(rays), mode=bzr.PIPELINE_FUSED)
     wo, ws, wg = orc.trace_chain([cfg2_lens], [1.3], rays)
     assert np.array_equal(u32(fo), u32(wo)) and np.array_equal(u32(fs), u32(ws)) and np.array_equal(u32(fg), u32(wg))
+
+
+@pytest.mark.parametrize("name,side", [("cfg3", 2048), ("cfg4", 4096), ("cfg5", 4096)])
+def test_full_size_fused_equals_staged(bzr, name, side):
+    """The two culled pipelines are independent implementations of the same selection (k_trace's in-wave
+    collected passes vs the staged pair buckets); at the configs' full sizes every output
+    word of every ray agrees (cfg5: 4096^2 of its 8192^2 grid, the bench's one-GPU size of round 1)."""
+    torch = pytest.importorskip("torch")
+    cfg = CONFIGS[name]
+    patches = [build_lens(bzr.TriMesh, l).bezier_patches() for l in cfg.lenses]
+    ctx = bzr.Context(0)
+    ctx.use_torch_stream()
+    dms = [bzr.DeviceMesh(ctx, p) for p in patches]
+    rays = torch.from_numpy(grid_rays(cfg, side=side)).cuda()
+    if cfg.op == "chain":
+        f = bzr.trace_chain(ctx, dms, [l.ri for l in cfg.lenses], rays, mode=bzr.PIPELINE_FUSED)
+        s = bzr.trace_chain(ctx, dms, [l.ri for l in cfg.lenses], rays, mode=bzr.PIPELINE_STAGED)
+        torch.cuda.synchronize()
+        for a, b in zip(f, s):
+            assert torch.equal(a.view(torch.int32), b.view(torch.int32))
+        assert int(f[2].sum()) > 2.5 * rays.shape[1]
+    else:
+        f = bzr.intersect(ctx, dms[0], rays, mode=bzr.PIPELINE_FUSED)
+        s = bzr.intersect(ctx, dms[0], rays, mode=bzr.PIPELINE_STAGED)
+        torch.cuda.synchronize()
+        assert torch.equal(f.view(torch.int32), s.view(torch.int32))
+        assert int((f[11].view(torch.int32) == 4).sum()) > rays.shape[1] // 10  # hits (what == intersect)
