@@ -16,7 +16,7 @@ weak: the image grows to side x (side*N).  Each frame's results are gathered to 
 the timed region, double-buffered so frame k's gather overlaps frame k+1's tracing: --gather image
 (default) the per-primary status + segment-count word (4 B; the final rays stay in each rank's HBM),
 --gather rays the final rays too (28 B per primary), --gather none nothing (tracing alone).
---inflight F (default 2): frame k runs on slot k % F (its own context, stream and output buffers), so
+--inflight F (default 3): frame k runs on slot k % F (its own context, stream and output buffers), so
 the next frame's waves fill the GPU while a frame's slowest waves finish; every frame is traced in full.
 
 Prints ONE JSON line on rank 0; fields are described in DESIGN.md (d).
@@ -32,6 +32,14 @@ import time
 from pathlib import Path
 
 import numpy as np
+
+# Frames in flight (--inflight) need their slot streams on distinct hardware queues.  HIP shares its
+# GPU_MAX_HW_QUEUES (default 4) queues among all streams of the process, and which streams end up sharing
+# depends on the creation / first-use order (torch's pool, the contexts' own streams, RCCL's): with 4, a
+# probe that created its streams in another order saw two slots land on one queue and lose the overlap
+# entirely.  16 queues give every stream here its own.  Set before HIP initialises (torch is imported
+# in main()).
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("BZR_BENCH_HW_QUEUES", "16")
 
 REPO = Path(__file__).resolve().parent
 sys.path.insert(0, str(REPO / "cuda-bezier-triangle-raytracer_amd"))
@@ -60,7 +68,7 @@ def parse():
     p.add_argument("--pipeline", default="fused", choices=["fused", "staged", "auto"],
                    help="culled-path pipeline (include/bzr.h BZR_PIPELINE_*; same output bits): fused = one k_trace "
                         "kernel per frame (default), staged = the multi-kernel path, auto = the library's choice")
-    p.add_argument("--inflight", type=int, default=2,
+    p.add_argument("--inflight", type=int, default=3,
                    help="frames in flight (each on its own context, stream and output buffers)")
     p.add_argument("--mode", default="parity", choices=["parity", "fast"],
                    help="fast = BZR_MODE_FAST Newton stage (contracted FMA, approximate div/sqrt; not bit-exact)")
@@ -198,8 +206,8 @@ def main():
     t0 = time.perf_counter()
     meshes = [bzr_amd.DeviceMesh(ctx, p) for p in patches]  # upload + BVH build
     upload_s = time.perf_counter() - t0
-    # one stream per frame slot (--inflight), created back to back: torch hands out its pooled streams
-    # round-robin, and consecutive ones sit on different hardware queues, so the slots' frames overlap
+    # one stream per frame slot (--inflight); GPU_MAX_HW_QUEUES (top of this file) gives each its own
+    # hardware queue, so the slots' frames overlap
     streams = [torch.cuda.Stream(dev) for _ in range(max(1, a.inflight))]
     stream = streams[0]  # slot 0: the kernels, torch ops and the timing events
     torch.cuda.set_stream(stream)

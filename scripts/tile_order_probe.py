@@ -20,12 +20,12 @@ K = 20
 cfg = CONFIGS["cfg4"]
 side = 4096
 patches = [build_lens(bzr_amd.TriMesh, l).bezier_patches() for l in cfg.lenses]
-ctx = bzr_amd.Context(0)
-ctx2 = bzr_amd.Context(0)
-stream, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+slot_ctx = [bzr_amd.Context(0) for _ in range(3)]
+slot_streams = [torch.cuda.Stream() for _ in range(3)]  # back to back: distinct hardware queues
+for c, st in zip(slot_ctx, slot_streams):
+    c.use_torch_stream(st)
+ctx, stream = slot_ctx[0], slot_streams[0]
 torch.cuda.set_stream(stream)
-ctx.use_torch_stream(stream)
-ctx2.use_torch_stream(s2)
 meshes = [bzr_amd.DeviceMesh(ctx, p) for p in patches]
 ris = [l.ri for l in cfg.lenses]
 mode = bzr_amd.MODE_PARITY | bzr_amd.PIPELINE_FUSED
@@ -94,28 +94,30 @@ for world in (1, 2, 4, 8):
             torch.cuda.synchronize()
             times.append(e0.elapsed_time(e1) / K)
         res[name] = round(float(np.median(times)), 4)
-    # two frames in flight (second context + stream, own outputs), centre-first order
+    # F frames in flight (own context, stream, outputs each), centre-first order
     rr, cc = centre_first(rows, cols)
     rays = torch.from_numpy(rays_for(cfg, rr, cc, side)).cuda()
     n = rays.shape[1]
-    slots = [(ctx, stream), (ctx2, s2)]
-    bufs = [(torch.empty((6, n), dtype=torch.float32, device="cuda"), torch.empty(n, dtype=torch.int32, device="cuda"),
-             torch.empty(n, dtype=torch.int32, device="cuda")) for _ in range(2)]
-    times = []
-    for rep in range(3):
-        torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        s2.wait_event(e0)
-        for k in range(K):
-            c, st = slots[k % 2]
-            with torch.cuda.stream(st):
-                bzr_amd.trace_chain(c, meshes, ris, rays, *bufs[k % 2], mode=mode)
-        ev = torch.cuda.Event()
-        ev.record(s2)
-        stream.wait_event(ev)
-        e1.record(stream)
-        torch.cuda.synchronize()
-        times.append(e0.elapsed_time(e1) / K)
-    res["centre_inflight2"] = round(float(np.median(times)), 4)
+    for F in (2, 3):
+        bufs = [(torch.empty((6, n), dtype=torch.float32, device="cuda"), torch.empty(n, dtype=torch.int32, device="cuda"),
+                 torch.empty(n, dtype=torch.int32, device="cuda")) for _ in range(F)]
+        times = []
+        for rep in range(3):
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for st in slot_streams[1:F]:
+                st.wait_event(e0)
+            for k in range(K):
+                c, st = slot_ctx[k % F], slot_streams[k % F]
+                with torch.cuda.stream(st):
+                    bzr_amd.trace_chain(c, meshes, ris, rays, *bufs[k % F], mode=mode)
+            for st in slot_streams[1:F]:
+                ev = torch.cuda.Event()
+                ev.record(st)
+                stream.wait_event(ev)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            times.append(e0.elapsed_time(e1) / K)
+        res[f"centre_inflight{F}"] = round(float(np.median(times)), 4)
     print(json.dumps({"world": world, "rank0_rays": int(len(rows)), **res}), flush=True)
