@@ -159,16 +159,22 @@ __device__ __forceinline__ float div_unscaled(float a, float b, float y) {  // y
 #endif
 __device__ __forceinline__ f3 unit(f3 a, float z) {  // Eigen normalized() for z > 0: a / sqrt(z), three divisions
 #if BZR_UNIT_SHARED
+  // the plain chain for every lane; lanes outside the guard redo it with the full sequences (the branch
+  // is rarely taken, and the common path then needs no copies at the join)
+  const float s = sqrt_unscaled(z);
+  const float y0 = __builtin_amdgcn_rcpf(s);
+  const float y = __builtin_fmaf(__builtin_fmaf(-s, y0, 1.0f), y0, y0);
+  f3 r = mk(div_unscaled(a.x, s, y), div_unscaled(a.y, s, y), div_unscaled(a.z, s, y));
   const float m = fminf(fminf(fabsf(a.x), fabsf(a.y)), fabsf(a.z));
-  if (m >= 0x1p-100f && z >= 0x1p-96f && z <= 0x1p40f) {
-    const float s = sqrt_unscaled(z);
-    const float y0 = __builtin_amdgcn_rcpf(s);
-    const float y = __builtin_fmaf(__builtin_fmaf(-s, y0, 1.0f), y0, y0);
-    return mk(div_unscaled(a.x, s, y), div_unscaled(a.y, s, y), div_unscaled(a.z, s, y));
+  if (!(m >= 0x1p-100f && z >= 0x1p-96f && z <= 0x1p40f)) {
+    const float sr = sqrt_rn(z);
+    r = mk(div_rn(a.x, sr), div_rn(a.y, sr), div_rn(a.z, sr));
   }
-#endif
+  return r;
+#else
   float s = sqrt_rn(z);
   return mk(div_rn(a.x, s), div_rn(a.y, s), div_rn(a.z, s));
+#endif
 }
 #include "patch_math_body.inc"
 }  // namespace exact
