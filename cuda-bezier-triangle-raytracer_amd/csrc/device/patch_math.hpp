@@ -136,7 +136,7 @@ __device__ __forceinline__ float sqrt_rn(float a) { return __builtin_sqrtf(a); }
 // Where v_div_scale scales nothing and v_div_fixup passes the quotient through, the plain fma chain is
 // the same instructions on the same values, so it returns the same correctly rounded bits.  V_DIV_SCALE
 // scales when: num or den is 0; exp(num) - exp(den) >= 96; den is denormal; 1/den or num/den is
-// denormal; |num| < 2^-103.  unit() takes the plain chain only when |a_k| >= 2^-100 for every k and
+// denormal; |num| < 2^-103.  unit_or_self() takes the plain chain only when |a_k| >= 2^-100 for every k and
 // 2^-96 <= z <= 2^40 (so s = sqrt(z) is in [2^-48, 2^20] and |a_k| / s >= 2^-120 is normal; |a_k| <= ~s):
 // none of those cases, no sqrt scaling, no special value.  The three quotients share the divisor, so
 // they share the reciprocal: 1 sqrt + 3 + 3 x 5 instructions instead of 1 + 3 x 11.
@@ -157,21 +157,26 @@ __device__ __forceinline__ float div_unscaled(float a, float b, float y) {  // y
 #ifndef BZR_UNIT_SHARED
 #define BZR_UNIT_SHARED 1
 #endif
-__device__ __forceinline__ f3 unit(f3 a, float z) {  // Eigen normalized() for z > 0: a / sqrt(z), three divisions
+// Eigen normalized() with z = a.a: a / sqrt(z) when z > 0, else a unchanged.
+__device__ __forceinline__ f3 unit_or_self(f3 a, float z) {
 #if BZR_UNIT_SHARED
-  // the plain chain for every lane; lanes outside the guard redo it with the full sequences (the branch
-  // is rarely taken, and the common path then needs no copies at the join)
+  // the plain chain for every lane; lanes outside the guard (z <= 0 among them) redo it with the full
+  // sequences or keep a (the branch is rarely taken, and the common path needs no copies at the join)
   const float s = sqrt_unscaled(z);
   const float y0 = __builtin_amdgcn_rcpf(s);
   const float y = __builtin_fmaf(__builtin_fmaf(-s, y0, 1.0f), y0, y0);
   f3 r = mk(div_unscaled(a.x, s, y), div_unscaled(a.y, s, y), div_unscaled(a.z, s, y));
   const float m = fminf(fminf(fabsf(a.x), fabsf(a.y)), fabsf(a.z));
   if (!(m >= 0x1p-100f && z >= 0x1p-96f && z <= 0x1p40f)) {
-    const float sr = sqrt_rn(z);
-    r = mk(div_rn(a.x, sr), div_rn(a.y, sr), div_rn(a.z, sr));
+    r = a;
+    if (z > 0.0f) {
+      const float sr = sqrt_rn(z);
+      r = mk(div_rn(a.x, sr), div_rn(a.y, sr), div_rn(a.z, sr));
+    }
   }
   return r;
 #else
+  if (!(z > 0.0f)) return a;
   float s = sqrt_rn(z);
   return mk(div_rn(a.x, s), div_rn(a.y, s), div_rn(a.z, s));
 #endif
@@ -184,7 +189,8 @@ namespace fast {
 #pragma clang fp contract(fast)
 __device__ __forceinline__ float div_rn(float a, float b) { return a * __builtin_amdgcn_rcpf(b); }
 __device__ __forceinline__ float sqrt_rn(float a) { return __builtin_amdgcn_sqrtf(a); }
-__device__ __forceinline__ f3 unit(f3 a, float z) {
+__device__ __forceinline__ f3 unit_or_self(f3 a, float z) {
+  if (!(z > 0.0f)) return a;
   float r = __builtin_amdgcn_rsqf(z);
   return mk(a.x * r, a.y * r, a.z * r);
 }

@@ -2151,7 +2151,7 @@ extern "C" bzr_status bzr_trace_chain(bzr_ctx *ctx, const bzr_mesh *const *lense
 
 // ------------------------------------------------------------ test hook: normalized()
 namespace {
-// Row k of out (k < 3): the product's exact normalized() (patch_math.hpp unit, shared-reciprocal chain
+// Row k of out (k < 3): the product's exact normalized() (patch_math.hpp unit_or_self, shared-reciprocal chain
 // where its guard allows); rows 3..5: sqrt_rn / div_rn per component (the compiler's own lowering).
 __global__ __launch_bounds__(kBlock) void k_debug_unit(const float *__restrict__ a, uint32_t n,
                                                        float *__restrict__ out) {
