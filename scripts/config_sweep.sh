@@ -7,7 +7,7 @@ OUT=gpurun_out/config_sweep.jsonl
 : > "$OUT"
 for spec in "cfg2 fused" "cfg2 staged" "cfg3 fused" "cfg3 staged" "cfg4 fused" "cfg4 staged" "cfg5 fused" "cfg5 staged"; do
   set -- $spec
-  for f in 1 2; do
+  for f in ${INFLIGHTS:-1 2 3}; do
     timeout -k 10 240 python bench.py --config "$1" --pipeline "$2" --inflight "$f" --steps ${STEPS:-10} --warmup 2 \
       --cpu-baseline off > gpurun_out/sweep_one.log 2>&1
     rc=$?
