@@ -16,7 +16,7 @@ weak: the image grows to side x (side*N).  Each frame's results are gathered to 
 the timed region, double-buffered so frame k's gather overlaps frame k+1's tracing: --gather image
 (default) the per-primary status + segment-count word (4 B; the final rays stay in each rank's HBM),
 --gather rays the final rays too (28 B per primary), --gather none nothing (tracing alone).
---inflight F (default 3): frame k runs on slot k % F (its own context, stream and output buffers), so
+--inflight F (default 3 for the fused pipeline, 2 otherwise): frame k runs on slot k % F (its own context, stream and output buffers), so
 the next frame's waves fill the GPU while a frame's slowest waves finish; every frame is traced in full.
 
 Prints ONE JSON line on rank 0; fields are described in DESIGN.md (d).
@@ -68,8 +68,9 @@ def parse():
     p.add_argument("--pipeline", default="fused", choices=["fused", "staged", "auto"],
                    help="culled-path pipeline (include/bzr.h BZR_PIPELINE_*; same output bits): fused = one k_trace "
                         "kernel per frame (default), staged = the multi-kernel path, auto = the library's choice")
-    p.add_argument("--inflight", type=int, default=3,
-                   help="frames in flight (each on its own context, stream and output buffers)")
+    p.add_argument("--inflight", type=int, default=0,
+                   help="frames in flight (each on its own context, stream and output buffers); "
+                        "0 = 3 for the fused pipeline, 2 otherwise (scripts/config_sweep.sh)")
     p.add_argument("--mode", default="parity", choices=["parity", "fast"],
                    help="fast = BZR_MODE_FAST Newton stage (contracted FMA, approximate div/sqrt; not bit-exact)")
     p.add_argument("--cpu-baseline", default="on", choices=["on", "off"])
@@ -208,6 +209,8 @@ def main():
     upload_s = time.perf_counter() - t0
     # one stream per frame slot (--inflight); GPU_MAX_HW_QUEUES (top of this file) gives each its own
     # hardware queue, so the slots' frames overlap
+    if a.inflight <= 0:  # the staged pipeline's small kernels contend beyond two frames
+        a.inflight = 3 if (a.accel == "bvh" and a.pipeline == "fused") else 2
     streams = [torch.cuda.Stream(dev) for _ in range(max(1, a.inflight))]
     stream = streams[0]  # slot 0: the kernels, torch ops and the timing events
     torch.cuda.set_stream(stream)
