@@ -154,6 +154,11 @@ __device__ __forceinline__ float div_unscaled(float a, float b, float y) {  // y
   r = __builtin_fmaf(-b, q, a);
   return __builtin_fmaf(r, y, q);
 }
+// newton_tail's acceptance test norm(perp) > 0.01f (reference/bezierTriangle.cpp:165) without the square
+// root: RN(sqrt(z)) is monotone in z, so RN(sqrt(z)) > 0.01f exactly when z > 0x38d1b718 (1.00000005e-4f),
+// the largest float whose correctly rounded square root is <= 0.01f -- checked over all 2^32 float bit
+// patterns, NaN and negatives included (tests/test_sqrt_threshold.py repeats it on a sample).
+__device__ __forceinline__ bool sqrt_above_hundredth(float z) { return z > __uint_as_float(0x38d1b718u); }
 #ifndef BZR_UNIT_SHARED
 #define BZR_UNIT_SHARED 1
 #endif
@@ -189,6 +194,7 @@ namespace fast {
 #pragma clang fp contract(fast)
 __device__ __forceinline__ float div_rn(float a, float b) { return a * __builtin_amdgcn_rcpf(b); }
 __device__ __forceinline__ float sqrt_rn(float a) { return __builtin_amdgcn_sqrtf(a); }
+__device__ __forceinline__ bool sqrt_above_hundredth(float z) { return sqrt_rn(z) > 0.01f; }
 __device__ __forceinline__ f3 unit_or_self(f3 a, float z) {
   if (!(z > 0.0f)) return a;
   float r = __builtin_amdgcn_rsqf(z);
