@@ -38,8 +38,9 @@ import numpy as np
 # depends on the creation / first-use order (torch's pool, the contexts' own streams, RCCL's): with 4, a
 # probe that created its streams in another order saw two slots land on one queue and lose the overlap
 # entirely.  16 queues give every stream here its own.  Set before HIP initialises (torch is imported
-# in main()).
-os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("BZR_BENCH_HW_QUEUES", "16")
+# in main()).  A value the caller already exported is kept (and reported in config.hw_queues).
+_HWQ_SOURCE = "caller" if "GPU_MAX_HW_QUEUES" in os.environ else "bench.py default"
+os.environ.setdefault("GPU_MAX_HW_QUEUES", os.environ.get("BZR_BENCH_HW_QUEUES", "16"))
 
 REPO = Path(__file__).resolve().parent
 sys.path.insert(0, str(REPO / "cuda-bezier-triangle-raytracer_amd"))
@@ -212,6 +213,11 @@ def main():
     if a.inflight <= 0:  # the staged pipeline's small kernels contend beyond two frames
         a.inflight = 3 if (a.accel == "bvh" and a.pipeline == "fused") else 2
     streams = [torch.cuda.Stream(dev) for _ in range(max(1, a.inflight))]
+    hwq = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
+    if hwq < len(streams) + (1 if world > 1 else 0) and rank == 0:
+        print(f"bench.py: warning: GPU_MAX_HW_QUEUES={hwq} < {len(streams)} frame streams"
+              f"{' + the RCCL stream' if world > 1 else ''}: slots may share a hardware queue and lose the overlap",
+              file=sys.stderr, flush=True)
     stream = streams[0]  # slot 0: the kernels, torch ops and the timing events
     torch.cuda.set_stream(stream)
     ctx.use_torch_stream(stream)
@@ -399,6 +405,9 @@ def main():
                                   f"{rows * 4} B per primary ({a.gather})" if gather else ""),
                 "pipeline": a.pipeline,
                 "frames_in_flight": F,
+                "hw_queues": {"GPU_MAX_HW_QUEUES": hwq, "source": _HWQ_SOURCE,
+                              "streams": len(streams) + (1 if gather else 0),
+                              "ok": hwq >= len(streams) + (1 if gather else 0)},
                 "scan": "BVH-culled (bit-identical to brute force)" if a.accel == "bvh" else "brute force",
                 "numerics": "parity: bit-identical to the CPU oracle" if a.mode == "parity" else
                             "fast: exact planar gate, Newton stage with FMA + approximate div/sqrt (SURVEY 8c fast gates)",

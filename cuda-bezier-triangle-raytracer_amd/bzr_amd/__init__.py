@@ -100,6 +100,7 @@ _SIGS = {
     "bzr_bezier_interpolate": [_P, _I32, _P],
     "bzr_debug_unit": [_P, _P, _U32, _P],
     "bzr_debug_wave_clock": [_P, _P, _U32],
+    "bzr_debug_wave_clock_rate": [_P, _P, _U32],
 }
 _RET = {"bzr_last_error": ctypes.c_char_p, "bzr_abi_version": _I32}
 

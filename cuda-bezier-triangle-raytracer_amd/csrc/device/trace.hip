@@ -68,6 +68,8 @@ struct bzr_mesh {
   float4 *leaf_near;
   bzr_host::Bvh4ObbNode *obb;       // both tiers' wide-patch subtrees (oriented boxes, bvh.hpp)
   bzr_host::Bvh4ObbNode *obb_near;
+  float4 *always;   // 4 float4 per always-tested patch (bvh.hpp Bvh::always): planar record, index in the last word
+  uint32_t n_always;
   uint32_t nnodes;
   float s_max;      // far tier: origins beyond take the full scan
   float s_near;     // near tier: waves whose rays all start within it walk the tighter tree
@@ -102,6 +104,7 @@ struct bzr_ctx {
   unsigned long long *counters = nullptr;  // device [BZR_COUNTER_COUNT]
   unsigned long long *wave_clock = nullptr;  // test hook (bzr_debug_wave_clock): per k_trace wave, device
   uint32_t wave_clock_cap = 0;
+  bool wave_clock_real = false;  // bzr_debug_wave_clock_rate: also s_memrealtime (4 words per wave)
 };
 
 namespace {
@@ -114,7 +117,12 @@ constexpr uint32_t kMaxLenses = 8;
 #endif
 constexpr uint32_t kMaxCand = BZR_MAX_CAND;  // candidate list length per ray and segment
 constexpr uint32_t kOverflow = 0xFFFFu;  // count value: resolve with the full scan
-constexpr int kStack = 64;
+// Traversal stack entries per wave (LDS).  BZR_STACK (A/B and test knob): a tiny stack makes waves run out
+// mid-walk, which sends the affected lanes to the in-order full scan (tests/test_gpu_variants.py).
+#ifndef BZR_STACK
+#define BZR_STACK 64
+#endif
+constexpr int kStack = BZR_STACK;
 
 // 64-byte wave-uniform records read through the constant address space: one s_load_dwordx16 each
 typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
@@ -183,6 +191,8 @@ struct MeshView {
   const float4 *__restrict__ leaf_near;
   const bzr_host::Bvh4ObbNode *__restrict__ obb;
   const bzr_host::Bvh4ObbNode *__restrict__ obb_near;
+  const float4 *__restrict__ always;  // patches without a proven gate region: gate-tested by every wave-segment
+  uint32_t n_always;
   uint32_t n;
   float s_max;
   float s_near;
@@ -494,6 +504,12 @@ __device__ __forceinline__ void record(float *__restrict__ slot, uint32_t cap, u
   atomicMin(key, ((unsigned long long)t_order(h.t) << 32) | p);
 }
 
+// Word group g of a 64-byte leaf record (planar record, patch index in the last word): q0..q3 of the gate.
+__device__ __forceinline__ float4 leaf_q(const u32x16 &r, int g) {
+  return make_float4(__uint_as_float(r[4 * g]), __uint_as_float(r[4 * g + 1]), __uint_as_float(r[4 * g + 2]),
+                     g == 3 ? 0.0f : __uint_as_float(r[4 * g + 3]));
+}
+
 // Candidate search.  `alive` (optional): a ray is traced iff alive[off + i] != BZR_RR_NONE.
 // One wave's 64 rays i (lane l of the wave holds ray i); `stk` is the wave's LDS stack.
 __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__restrict__ rays, uint32_t ld,
@@ -549,6 +565,15 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
       }
     }
   }
+  // the always list (patches without a proven gate region, bvh.cpp): gate-tested for every active ray
+  if (__any(active))
+    for (uint32_t k = 0; k < m.n_always; ++k) {
+      const u32x16 r = *((const cu32x16 *)(uintptr_t)m.always + k);
+      if (active & planar_gate(leaf_q(r, 0), leaf_q(r, 1), leaf_q(r, 2), leaf_q(r, 3), s, d)) {
+        if (cnt < kMaxCand) w.cand[(size_t)cnt * n + i] = r[15];
+        cnt = cnt < kMaxCand ? cnt + 1 : kOverflow;
+      }
+    }
   if (count_rays) {  // rays traced (one atomic per wave: on one address, so only with counters on)
     const unsigned long long traced = __ballot(i < n && (alive == nullptr || alive[off + i] != BZR_RR_NONE));
     if ((threadIdx.x & 63u) == 0 && traced) atomicAdd(&w.ctr[2], (uint32_t)__popcll(traced));
@@ -1071,6 +1096,7 @@ __device__ __forceinline__ void trace_segment(const MeshView &m, f3 s, f3 d, boo
   uint32_t scan = kNo;                // next patch of the full scan (kNo: not scanning)
   uint32_t join = kNo, join_src = 0;  // a retry waiting for a later leaf's pass: that leaf, scanned patch
   uint32_t parked_nb = kNo;           // the patch whose cNone result is parked for this lane
+  uint32_t ai = __any(act) ? 0u : m.n_always;  // next always-list record (uniform)
   for (;;) {
     uint32_t ne = 0;  // collected leaves (uniform)
 #if BZR_TRACE_PRIO
@@ -1114,6 +1140,24 @@ __device__ __forceinline__ void trace_segment(const MeshView &m, f3 s, f3 d, boo
           next = ch[c];
           next_hm = hm;
         }
+      }
+    }
+    // tree done: the always list (patches without a proven gate region, bvh.cpp), gate-tested by every
+    // wave-segment -- the candidates no box may cull
+    for (; next == kNo && sp == 0 && ai < m.n_always && ne < kEntries; ++ai) {
+      const u32x16 r = *((const cu32x16 *)(uintptr_t)m.always + ai);
+      const bool pass = act & planar_gate(leaf_q(r, 0), leaf_q(r, 1), leaf_q(r, 2), leaf_q(r, 3), s, d);
+      if (kCount) {
+        ++ctr.leaves;
+        ctr.gate_tests += popc64(__ballot(act));
+      }
+      const unsigned long long pm = __ballot(pass);
+      if (pm) {
+        if (lane == 0u) {
+          L.eid[ne] = r[15];
+          L.emask[ne] = pm;
+        }
+        ++ne;
       }
     }
     if (ne == 0u) {  // tree done: the reference's in-order scan for the lanes that could not use it
@@ -1228,6 +1272,7 @@ struct TraceJob {
   uint32_t n;
   uint32_t ld;               // row stride of rays / out_rays / hits (>= n)
   unsigned long long *wave_clock;  // optional test hook: [2 * waves] start, duration (s_memtime ticks)
+  uint32_t wave_real;              // wave_clock holds [4 * waves]: + s_memrealtime start, duration (100 MHz)
 };
 
 // BZR_TRACE_WPE (A/B knob, default 0 = the compiler's choice): amdgpu_waves_per_eu lower bound for k_trace.
@@ -1264,6 +1309,7 @@ __global__ __launch_bounds__(kTraceBlock) BZR_TRACE_ATTR void k_trace(LensSet le
   TraceLds<kMode> &L = lds[threadIdx.x >> 6];
   const uint32_t i = trace_tile(blockIdx.x, gridDim.x) * kTraceBlock + threadIdx.x;
   const unsigned long long t_start = job.wave_clock ? __builtin_amdgcn_s_memtime() : 0ull;
+  const unsigned long long r_start = (job.wave_clock && job.wave_real) ? __builtin_amdgcn_s_memrealtime() : 0ull;
   const uint32_t n = job.n;
   TraceCtr ctr;
   bool alive = i < n;
@@ -1307,8 +1353,16 @@ __global__ __launch_bounds__(kTraceBlock) BZR_TRACE_ATTR void k_trace(LensSet le
   }
   if (job.wave_clock && lane == 0u) {  // the wave's tile (ray index / 64): start tick and duration
     const unsigned long long t_end = __builtin_amdgcn_s_memtime();
-    job.wave_clock[2 * (i >> 6)] = t_start;
-    job.wave_clock[2 * (i >> 6) + 1] = t_end - t_start;
+    if (job.wave_real) {  // diagnostic: the wave's shader clock = d(s_memtime) / d(s_memrealtime) x 100 MHz
+      const unsigned long long r_end = __builtin_amdgcn_s_memrealtime();
+      job.wave_clock[4 * (i >> 6)] = t_start;
+      job.wave_clock[4 * (i >> 6) + 1] = t_end - t_start;
+      job.wave_clock[4 * (i >> 6) + 2] = r_start;
+      job.wave_clock[4 * (i >> 6) + 3] = r_end - r_start;
+    } else {
+      job.wave_clock[2 * (i >> 6)] = t_start;
+      job.wave_clock[2 * (i >> 6) + 1] = t_end - t_start;
+    }
   }
   if (kCount && lane < 8u) {  // one atomic per counter per wave, spread over kCounterReplicas copies
     const uint32_t v[8] = {ctr.segments, ctr.pairs, ctr.follows, ctr.ovf, ctr.nodes, ctr.leaves, ctr.gate_tests,
@@ -1422,7 +1476,7 @@ struct DeviceGuard {
 
 MeshView view_of(const bzr_mesh *m, float ri = 1.0f) {
   return MeshView{m->planar, m->full, m->nodes, m->leaf, m->nodes_near, m->leaf_near, m->obb, m->obb_near,
-                  m->n, m->s_max, m->s_near, ri};
+                  m->always, m->n_always, m->n, m->s_max, m->s_near, ri};
 }
 unsigned grid_for(uint32_t n) { return (n + kBlock - 1) / kBlock; }
 size_t round256(size_t b) { return (b + 255) & ~size_t(255); }
@@ -1468,7 +1522,11 @@ bool use_staged(uint32_t flags, uint64_t n, uint64_t nb) {
   return n < kFusedRaysPerPatch * nb;
 }
 // BZR_MODE_FAST runs on the culled pipeline's kernels only; the brute-force scan is the parity reference.
+constexpr uint32_t kKnownFlags = BZR_DEVICE_PTRS | BZR_MODE_FAST | BZR_ACCEL_NONE | BZR_PIPELINE_STAGED | BZR_PIPELINE_FUSED;
 bzr_status check_flags(uint32_t flags) {
+  if (flags & ~kKnownFlags) return set_error(BZR_ERR_INVALID_ARGUMENT, "unknown flag bits " + std::to_string(flags & ~kKnownFlags));
+  if ((flags & BZR_PIPELINE_STAGED) && (flags & BZR_PIPELINE_FUSED))
+    return set_error(BZR_ERR_INVALID_ARGUMENT, "BZR_PIPELINE_STAGED and BZR_PIPELINE_FUSED are exclusive");
   if (use_fast(flags) && use_scan(flags))
     return set_error(BZR_ERR_INVALID_ARGUMENT, "BZR_MODE_FAST needs the culled path (drop BZR_ACCEL_NONE)");
   return BZR_OK;
@@ -1651,6 +1709,7 @@ bzr_status run_fused(bzr_ctx *ctx, const LensSet &set, const TraceJob &job, uint
   const dim3 grid((job.n + kTraceBlock - 1) / kTraceBlock), block(kTraceBlock);
   TraceJob j = job;
   j.wave_clock = (ctx->wave_clock && ctx->wave_clock_cap >= (job.n + 63) / 64) ? ctx->wave_clock : nullptr;
+  j.wave_real = ctx->wave_clock_real ? 1u : 0u;
   auto go = [&](auto kernel) { launch_on(ctx, ctx->stream, block, BZR_KERNEL_TRACE, kernel, grid, set, j, ctx->counters); };
   if (fast) {
     if (count) go(k_trace<kMode, true, true>);
@@ -1862,11 +1921,21 @@ extern "C" bzr_status bzr_mesh_create(bzr_ctx *ctx, const void *patches, uint32_
     return leaf;
   };
   const std::vector<float4> leaf = leaves(bvh), leaf_near = leaves(bvh_near);
+  // the always list: the same patches in both tiers (whether a gate region is proven does not depend on
+  // the tier's origin radius)
+  if (bvh.always != bvh_near.always) return set_error(BZR_ERR_INVALID_ARGUMENT, "BVH tiers disagree on the always list");
+  std::vector<float4> always(bvh.always.size() * 4);
+  for (size_t k = 0; k < bvh.always.size(); ++k) {
+    const uint32_t b = bvh.always[k];
+    for (int j = 0; j < 4; ++j) always[4 * k + j] = planar[4 * b + j];
+    std::memcpy(&always[4 * k + 3].w, &b, 4);
+  }
   bzr_mesh *mesh = new (std::nothrow) bzr_mesh();
   if (!mesh) return set_error(BZR_ERR_OUT_OF_MEMORY, "mesh allocation");
   mesh->device = ctx->device;
   mesh->n = n;
   mesh->nnodes = static_cast<uint32_t>(bvh.nodes4.size());
+  mesh->n_always = static_cast<uint32_t>(bvh.always.size());
   mesh->s_max = bvh.s_max;
   mesh->s_near = std::min(bvh_near.s_max, bvh.s_max);
   for (int k = 0; k < 4; ++k) mesh->sphere[k] = bvh.sphere[k];
@@ -1885,6 +1954,7 @@ extern "C" bzr_status bzr_mesh_create(bzr_ctx *ctx, const void *patches, uint32_
       {reinterpret_cast<void **>(&mesh->obb), bvh.obb.data(), bvh.obb.size() * sizeof(bzr_host::Bvh4ObbNode)},
       {reinterpret_cast<void **>(&mesh->obb_near), bvh_near.obb.data(),
        bvh_near.obb.size() * sizeof(bzr_host::Bvh4ObbNode)},
+      {reinterpret_cast<void **>(&mesh->always), always.data(), always.size() * sizeof(float4)},
   };
   hipError_t e = hipSuccess;
   for (auto &u : ups) {
@@ -1913,6 +1983,7 @@ extern "C" bzr_status bzr_mesh_destroy(bzr_mesh *mesh) {
   (void)hipFree(mesh->leaf_near);
   (void)hipFree(mesh->obb);
   (void)hipFree(mesh->obb_near);
+  (void)hipFree(mesh->always);
   delete mesh;
   return BZR_OK;
 }
@@ -1925,8 +1996,8 @@ extern "C" bzr_status bzr_mesh_size(const bzr_mesh *mesh, uint32_t *n) {
 
 extern "C" bzr_status bzr_intersect(bzr_ctx *ctx, const bzr_mesh *mesh, const float *rays, uint32_t n, float *hits,
                                     uint32_t flags) {
-  if (bzr_status s = check_ctx_mesh(ctx, mesh)) return s;
   if (bzr_status s = check_flags(flags)) return s;
+  if (bzr_status s = check_ctx_mesh(ctx, mesh)) return s;
   if (n == 0) return BZR_OK;
   if (!rays || !hits) return set_error(BZR_ERR_INVALID_ARGUMENT, "null buffer");
   DeviceGuard g(ctx->device);
@@ -1971,8 +2042,8 @@ extern "C" bzr_status bzr_intersect(bzr_ctx *ctx, const bzr_mesh *mesh, const fl
 
 extern "C" bzr_status bzr_patch_intersect(bzr_ctx *ctx, const bzr_mesh *mesh, const uint32_t *idx, const uint32_t *limit,
                                           const float *rays, uint32_t n, float *hits, uint32_t flags) {
-  if (bzr_status s = check_ctx_mesh(ctx, mesh)) return s;
   if (bzr_status s = check_flags(flags)) return s;
+  if (bzr_status s = check_ctx_mesh(ctx, mesh)) return s;
   if (n == 0) return BZR_OK;
   if (!idx || !limit || !rays || !hits) return set_error(BZR_ERR_INVALID_ARGUMENT, "null buffer");
   DeviceGuard g(ctx->device);
@@ -2009,8 +2080,8 @@ extern "C" bzr_status bzr_patch_intersect(bzr_ctx *ctx, const bzr_mesh *mesh, co
 extern "C" bzr_status bzr_refract(bzr_ctx *ctx, const bzr_mesh *mesh, float ri, const float *rays, const uint32_t *expected,
                                   uint32_t expected_all, uint32_t n, float *out_rays, uint32_t *out_status,
                                   uint32_t flags) {
-  if (bzr_status s = check_ctx_mesh(ctx, mesh)) return s;
   if (bzr_status s = check_flags(flags)) return s;
+  if (bzr_status s = check_ctx_mesh(ctx, mesh)) return s;
   if (n == 0) return BZR_OK;
   if (!rays || !out_rays || !out_status) return set_error(BZR_ERR_INVALID_ARGUMENT, "null buffer");
   DeviceGuard g(ctx->device);
@@ -2071,10 +2142,10 @@ extern "C" bzr_status bzr_refract(bzr_ctx *ctx, const bzr_mesh *mesh, float ri, 
 extern "C" bzr_status bzr_trace_chain(bzr_ctx *ctx, const bzr_mesh *const *lenses, const float *ri, uint32_t nlens,
                                       const float *rays, uint32_t n, float *out_rays, uint32_t *out_status,
                                       uint32_t *out_segments, uint32_t flags) {
+  if (bzr_status s = check_flags(flags)) return s;
   if (!ctx) return set_error(BZR_ERR_INVALID_ARGUMENT, "null context");
   if (nlens == 0 || nlens > kMaxLenses) return set_error(BZR_ERR_INVALID_ARGUMENT, "nlens must be 1..8");
   if (!lenses || !ri) return set_error(BZR_ERR_INVALID_ARGUMENT, "null lens list");
-  if (bzr_status s = check_flags(flags)) return s;
   LensSet set{};
   set.count = nlens;
   for (uint32_t l = 0; l < nlens; ++l) {
@@ -2176,6 +2247,16 @@ extern "C" bzr_status bzr_debug_wave_clock(void *ctxp, unsigned long long *clock
   if (!ctx) return set_error(BZR_ERR_INVALID_ARGUMENT, "null context");
   ctx->wave_clock = clock;
   ctx->wave_clock_cap = clock ? waves : 0u;
+  ctx->wave_clock_real = false;
+  return BZR_OK;
+}
+
+extern "C" bzr_status bzr_debug_wave_clock_rate(void *ctxp, unsigned long long *clock, uint32_t waves) {
+  bzr_ctx *ctx = static_cast<bzr_ctx *>(ctxp);
+  if (!ctx) return set_error(BZR_ERR_INVALID_ARGUMENT, "null context");
+  ctx->wave_clock = clock;
+  ctx->wave_clock_cap = clock ? waves : 0u;
+  ctx->wave_clock_real = clock != nullptr;
   return BZR_OK;
 }
 
@@ -2217,8 +2298,8 @@ __global__ __launch_bounds__(kBlock) void k_tessellate(const float *__restrict__
 
 extern "C" bzr_status bzr_mesh_interpolate(bzr_ctx *ctx, const bzr_mesh *mesh, int32_t divisor, float *out_xyz,
                                            uint32_t flags) {
-  if (bzr_status s = check_ctx_mesh(ctx, mesh)) return s;
   if (bzr_status s = check_flags(flags)) return s;
+  if (bzr_status s = check_ctx_mesh(ctx, mesh)) return s;
   if (divisor < 1 || divisor > 4096) return set_error(BZR_ERR_INVALID_ARGUMENT, "divisor must be 1..4096");
   const uint32_t K = static_cast<uint32_t>(divisor) * static_cast<uint32_t>(divisor);
   const uint64_t total = (uint64_t)K * mesh->n;

@@ -19,6 +19,7 @@
 #include <cmath>
 #include <cstring>
 #include <numeric>
+#include <stdexcept>
 
 namespace bzr_host {
 namespace {
@@ -44,8 +45,8 @@ double normd(d3 a) { return std::sqrt(dotd(a, a)); }
 //           (t = fma(lo, 1/d, -s/d): ~4 u (X + s_max) in space): 16 u (X + s_max), 2x the sum
 //   kSlack  the barycentric slack: fl(M_k p) differs from M_k p by at most gamma_3 sum_l |M_kl| |p_l|
 //           (gamma_3 = 3.0000002 u) -- 2^-21 = 8 u is 2.7x that (proven allowance, see gate_region_box)
-//   kRound1 round 1's allowance, 2^-18 = 64 u, kept for the barycentric slack of the rounding-dominated
-//           patches, whose gate no bound covers (checked empirically)
+// The rounding-dominated patches, whose gate no bound covers, get no box at all: they are left out of
+// the tree and gate-tested by every wave-segment (Bvh::always), so culling is exact by construction.
 #ifndef BZR_BVH_EPS_U
 #define BZR_BVH_EPS_U 24.0
 #endif
@@ -58,10 +59,6 @@ double normd(d3 a) { return std::sqrt(dotd(a, a)); }
 constexpr double kEps = BZR_BVH_EPS_U / 16777216.0;
 constexpr double kPad = BZR_BVH_PAD_U / 16777216.0;
 constexpr double kSlack = 1.0 / (1 << BZR_BVH_KSLACK_LOG2);
-#ifndef BZR_BVH_ROUND1_LOG2
-#define BZR_BVH_ROUND1_LOG2 18
-#endif
-constexpr double kRound1 = 1.0 / (1 << BZR_BVH_ROUND1_LOG2);
 
 // Clip convex polygon `poly` (plane points) to { x : g.x + h >= 0 }.
 std::vector<d3> clip(std::vector<d3> const &poly, d3 g, double h) {
@@ -87,6 +84,7 @@ std::vector<d3> clip(std::vector<d3> const &poly, d3 g, double h) {
 struct Region {       // the gate region's extreme points (double) and the ray-point padding
   enum Kind { kEmpty, kFinite, kUnbounded };
   Kind kind = kUnbounded;  // kEmpty: never a candidate; kUnbounded: non-finite record data
+  bool proven = false;     // the region is a proven bound (else: the patch goes to the always list)
   std::vector<d3> pts;
   double pad = 0.0;
 };
@@ -136,8 +134,9 @@ Box gate_region_box(const float *rec, double s_max, Region *region = nullptr) {
   // slack_k = kSlack (sum_l |M_kl| P_l + 1) (kSlack = 2.7 gamma_3) is a proven allowance; X = max(max P,
   // ext) bounds |p|_inf.  |Q| is the double-precision inverse widened by its residual.  Otherwise (the
   // rounding-dominated patches: the rows of M nearly parallel to the normal, fl(M p) is rounding noise
-  // near the plane) the patch keeps round 1's allowance kRound1 (l1_k ext + 1), checked
-  // empirically (tests/test_culling_conservative.py, tests/test_gpu_parity.py culled == brute force).
+  // near the plane) no bound exists -- along M's near-null direction the noise of fl(M p)
+  // grows with |p| and can land in [0,1]^3 arbitrarily far out -- so the patch gets no box: it returns
+  // the always-hit box with region->proven false, and build_bvh moves it to the always list.
   const double g3 = 3.0000002 / 16777216.0;
   double rn = 0.0;  // max column sum of |I - M Q~|
   for (int j = 0; j < 3; ++j) {
@@ -179,14 +178,13 @@ Box gate_region_box(const float *rec, double s_max, Region *region = nullptr) {
       if (!std::isfinite(P[i])) proven = false;
     }
   }
-  const double X = proven ? std::max({ext, P[0], P[1], P[2]}) : ext;
+  if (!proven) return all;
+  const double X = std::max({ext, P[0], P[1], P[2]});
   if (!std::isfinite(X)) return all;
+  if (region) region->proven = true;
   double slack[3];
-  for (int k = 0; k < 3; ++k) {
-    const double l1 = std::fabs(row[k][0]) + std::fabs(row[k][1]) + std::fabs(row[k][2]);
-    slack[k] = proven ? kSlack * (std::fabs(row[k][0]) * P[0] + std::fabs(row[k][1]) * P[1] + std::fabs(row[k][2]) * P[2] + 1.0)
-                      : kRound1 * (l1 * X + 1.0);
-  }
+  for (int k = 0; k < 3; ++k)
+    slack[k] = kSlack * (std::fabs(row[k][0]) * P[0] + std::fabs(row[k][1]) * P[1] + std::fabs(row[k][2]) * P[2] + 1.0);
   const double eps = kEps * (X + s_max);  // off-plane distance of the float plane point
   std::vector<d3> pts;
   // the initial square must contain the whole slab slice of the slack-inflated parallelepiped
@@ -640,12 +638,19 @@ Bvh build_bvh(const float *records, uint32_t n, uint32_t stride_words, int tier)
   if (!std::isfinite(out.extent)) out.extent = HUGE_VALF;
   out.order.resize(n);
   std::iota(out.order.begin(), out.order.end(), 0u);
+  // Patches without a proven gate region (rounding-dominated or non-finite records) leave the tree for the
+  // always list: order = [tree slots..., always...], the tree is built over the first n_tree slots.
+  {
+    auto mid = std::stable_partition(out.order.begin(), out.order.end(), [&](uint32_t i) { return region[i].proven; });
+    out.always.assign(mid, out.order.end());
+  }
+  const uint32_t n_tree = n - static_cast<uint32_t>(out.always.size());
   // Wide patches: gate regions much larger than their own triangle (planes through or near the
   // origin make M ill-conditioned).  Mixed into the tree their boxes would inflate
   // every ancestor's box and send most rays into those subtrees, so they get a subtree of their own
   // beside the narrow patches' (root = (narrow, wide)).
-  uint32_t n_narrow = n;
-  if (n >= kWideMinPatches) {
+  uint32_t n_narrow = n_tree;
+  if (n_tree >= kWideMinPatches) {
     auto wide = [&](uint32_t i) {
       Box const &b = box[i];
       if (b.empty) return false;
@@ -658,11 +663,11 @@ Bvh build_bvh(const float *records, uint32_t n, uint32_t stride_words, int tier)
       }
       return !(ext <= kWideRatio * tri);  // also non-finite boxes
     };
-    auto mid = std::stable_partition(out.order.begin(), out.order.end(), [&](uint32_t i) { return !wide(i); });
+    auto mid = std::stable_partition(out.order.begin(), out.order.begin() + n_tree, [&](uint32_t i) { return !wide(i); });
     n_narrow = static_cast<uint32_t>(mid - out.order.begin());
   }
   ObbBuild ob;
-  if (n && n_narrow > 0 && n_narrow < n) {
+  if (n_tree && n_narrow > 0 && n_narrow < n_tree) {
     out.nodes.push_back({});  // root, filled below
     const uint32_t l = bld.build(0, n_narrow);
 // BZR_BVH_OBB (A/B knob, default 0): oriented boxes for the wide subtree (nodes over at most
@@ -676,7 +681,7 @@ Bvh build_bvh(const float *records, uint32_t n, uint32_t stride_words, int tier)
 #ifdef BZR_BVH_OBB_MAX
     ob.max_obb_patches = BZR_BVH_OBB_MAX;
 #endif
-    const uint32_t r = bld.build(n_narrow, n - n_narrow);
+    const uint32_t r = bld.build(n_narrow, n_tree - n_narrow);
     BvhNode root;
     for (int a = 0; a < 3; ++a) {
       root.lo[a] = std::min(out.nodes[l].lo[a], out.nodes[r].lo[a]);
@@ -685,16 +690,33 @@ Bvh build_bvh(const float *records, uint32_t n, uint32_t stride_words, int tier)
     root.a = l;
     root.b = r;
     out.nodes[0] = root;
-  } else if (n) {
-    bld.build(0, n);
+  } else if (n_tree) {
+    bld.build(0, n_tree);
   }
-  if (n) {
+  if (n_tree) {
     ob.range.resize(out.nodes.size());
     fill_ranges(out.nodes, 0, ob.range);
     ob.region = &region;
     ob.order = &out.order;
     ob.obb = &out.obb;
     collapse(out.nodes, 0, out.nodes4, ob);
+    // Exact by construction: every leaf the device can reach holds a patch with a proven gate region.
+    std::vector<uint32_t> todo{0u};
+    while (!todo.empty()) {
+      const uint32_t ref = todo.back();
+      todo.pop_back();
+      for (int c = 0; c < 4; ++c) {
+        const uint32_t ch = (ref & kObbFlag) ? out.obb[ref & ~kObbFlag].c[c].child : out.nodes4[ref].child[c];
+        if (ch == kEmptyChild) continue;
+        if (ch & kLeafFlag) {
+          const uint32_t slot = ch & ~kLeafFlag;
+          if (slot >= n_tree || !region[out.order[slot]].proven)
+            throw std::logic_error("BVH leaf without a proven gate region");
+        } else {
+          todo.push_back(ch);
+        }
+      }
+    }
   } else {
     Bvh4Node root{};
     for (int c = 0; c < 4; ++c) root.child[c] = kEmptyChild;
@@ -709,7 +731,7 @@ Bvh build_bvh(const float *records, uint32_t n, uint32_t stride_words, int tier)
   }
   out.patch_obb.assign((size_t)n * 16, 0.0f);
   if (ob.wide_first != 0xFFFFFFFFu)
-    for (uint32_t k = n_narrow; k < n; ++k) {  // the wide patches' own boxes (what their parents test)
+    for (uint32_t k = n_narrow; k < n_tree; ++k) {  // the wide patches' own boxes (what their parents test)
       const uint32_t p = out.order[k];
       if (region[p].kind == Region::kEmpty) continue;
       fit_obb(region[p].pts, 2.0 * region[p].pad, &out.patch_obb[(size_t)p * 16]);  // always-hit if unbounded
@@ -889,7 +911,27 @@ extern "C" int32_t bzr_debug_traverse(const void *patches, uint32_t n, uint32_t 
         }
       }
     }
+    for (uint32_t b : bvh.always) {  // gate-tested by every wave-segment (the kernel's always loop)
+      stats[1] += 1;
+      for (uint32_t l = 0; l < lanes; ++l)
+        if (active[l]) {
+          stats[2] += 1;
+          if (hits) hits[(size_t)(w0 + l) * n + b] = 1;
+        }
+    }
   }
+  return 0;
+}
+
+// The always list of one tier (patches without a proven gate region, ascending): count, and the indices
+// when `out` is not null.
+extern "C" int32_t bzr_debug_always_list(const void *patches, uint32_t n, uint32_t stride, int32_t tier, uint32_t *out,
+                                         uint32_t *count) {
+  if ((!patches && n) || !count || stride % 4 || stride < 264) return 1;
+  if (tier != bzr_host::kTierFar && tier != bzr_host::kTierNear) return 1;
+  bzr_host::Bvh bvh = bzr_host::build_bvh(static_cast<const float *>(patches), n, stride / 4, tier);
+  *count = static_cast<uint32_t>(bvh.always.size());
+  if (out) std::memcpy(out, bvh.always.data(), bvh.always.size() * sizeof(uint32_t));
   return 0;
 }
 

@@ -54,7 +54,10 @@ struct Bvh {
   std::vector<Bvh4ObbNode> obb;    // the wide subtree's nodes (refs kObbFlag | index)
   std::vector<float> patch_obb;    // per patch (mesh order): c, u, v, w, h (15 floats) + 1 if it has one
   std::vector<BvhNode> nodes;      // binary build tree (one patch per leaf), root = 0
-  std::vector<uint32_t> order;     // leaf ranges index this: patch index in mesh order
+  std::vector<uint32_t> order;     // leaf ranges index this: patch index in mesh order; the tree's slots
+                                   // are [0, n - always.size()), the always-tested patches follow
+  std::vector<uint32_t> always;    // patches whose gate region has no proven bound (bvh.cpp), ascending:
+                                   // not in the tree, every wave-segment gate-tests them
   std::vector<float> patch_box;    // per order slot: lo.xyz, 0, hi.xyz, 0 (the gate-region box)
   float extent = 0.0f;             // max |coordinate| of any finite box
   float s_max = 0.0f;              // rays with |origin|_inf > s_max take the brute-force path

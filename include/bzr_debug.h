@@ -14,6 +14,12 @@ int32_t bzr_debug_gate_boxes(const void *patches, uint32_t n, uint32_t stride, f
  * origins |s|_inf <= *s_max, which is 8x the mesh's control-point span). */
 int32_t bzr_debug_gate_boxes_tier(const void *patches, uint32_t n, uint32_t stride, int32_t tier, float *boxes,
                                   float *s_max);
+/* Patches without a proven gate region (rounding-dominated, or non-finite records): they are not in the
+ * tier's tree and every wave-segment gate-tests them (bvh.hpp Bvh::always).  *count = their number; out
+ * (optional, *count words) = their indices, ascending.  Their gate boxes above are the always-hit box.
+ * Returns 0 on success. */
+int32_t bzr_debug_always_list(const void *patches, uint32_t n, uint32_t stride, int32_t tier, uint32_t *out,
+                              uint32_t *count);
 /* The oriented gate-region boxes of one tier's wide-patch subtree (bvh.hpp Bvh4ObbNode), by patch index:
  * out[16*i] = centre xyz, axes u v w (xyz each), half extents (3), then 1.0f if patch i is a wide patch
  * (its parent node tests this box) or 0.0f (16 zeros: the patch is AABB-culled).  Returns 0 on success. */
@@ -38,6 +44,10 @@ int32_t bzr_debug_unit(void *ctx, const float *a, uint32_t n, float *out);
  * clock[2w+1] = its duration, for wave w = ray index / 64.  `clock` is device memory; NULL turns it off.
  * ctx is a bzr_ctx* (bzr.h). */
 int32_t bzr_debug_wave_clock(void *ctx, unsigned long long *clock, uint32_t waves);
+/* The same with the constant 100 MHz clock beside it (a diagnostic of the shader clock the chip holds,
+ * MI355X_MICROARCH.md "DVFS give-back" item 6): clock[4w] = start, [4w+1] = duration (s_memtime ticks),
+ * [4w+2] = start, [4w+3] = duration (s_memrealtime ticks); the wave's clock is [4w+1] / [4w+3] x 100 MHz. */
+int32_t bzr_debug_wave_clock_rate(void *ctx, unsigned long long *clock, uint32_t waves);
 #ifdef __cplusplus
 }
 #endif

@@ -55,6 +55,27 @@ def test_errors_are_status_codes(bzr):
         bzr.TriMesh().make_ellipsoid(4, 2).bezier_patches()
 
 
+def test_flags_are_validated_first(bzr):
+    """Unknown flag bits and both pipeline bits together are rejected before anything else (no device
+    needed): a caller's mistake fails loudly instead of silently picking one pipeline."""
+    L = bzr.lib()
+    bad = {bzr.PIPELINE_STAGED | bzr.PIPELINE_FUSED: b"exclusive", 1 << 7: b"unknown flag", 1 << 31: b"unknown flag",
+           bzr.MODE_FAST | bzr.ACCEL_NONE: b"culled path"}
+    f = (ctypes.c_float * 1)(1.3)
+    for flags, msg in bad.items():
+        assert L.bzr_intersect(None, None, None, 0, None, flags) == 1
+        assert msg in L.bzr_last_error(), (flags, L.bzr_last_error())
+        assert L.bzr_refract(None, None, ctypes.c_float(1.3), None, None, 0, 0, None, None, flags) == 1
+        assert msg in L.bzr_last_error()
+        assert L.bzr_trace_chain(None, None, f, 1, None, 0, None, None, None, flags) == 1
+        assert msg in L.bzr_last_error()
+    # every documented combination passes the flag check (and then fails on the null context)
+    for flags in (0, bzr.DEVICE_PTRS, bzr.MODE_FAST, bzr.ACCEL_NONE, bzr.PIPELINE_STAGED, bzr.PIPELINE_FUSED,
+                  bzr.DEVICE_PTRS | bzr.MODE_FAST | bzr.PIPELINE_FUSED):
+        assert L.bzr_intersect(None, None, None, 0, None, flags) == 1
+        assert b"null context" in L.bzr_last_error()
+
+
 def test_trace_tiled_validates_before_touching_a_device(bzr):
     import ctypes
     L = bzr.lib()

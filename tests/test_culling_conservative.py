@@ -253,12 +253,62 @@ def test_ill_conditioned_patches_never_culled(bzr, orc, tier):
     assert passes > 200 and dominated_passes > 150
 
 
+def always_list(bzr, patches, tier):
+    L = bzr.lib()
+    fn = L.bzr_debug_always_list
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p]
+    fn.restype = ctypes.c_int32
+    p = np.ascontiguousarray(patches, np.float32)
+    cnt = np.zeros(1, np.uint32)
+    assert fn(p.ctypes.data, len(p), 264, tier, None, cnt.ctypes.data) == 0
+    out = np.zeros(int(cnt[0]), np.uint32)
+    assert fn(p.ctypes.data, len(p), 264, tier, out.ctypes.data, cnt.ctypes.data) == 0
+    return out
+
+
 @pytest.mark.parametrize("cfg_name,expect", [("cfg1", 0), ("cfg2", 0), ("cfg3", 0), ("cfg5", 126)])
-def test_rounding_dominated_counts(bzr, cfg_name, expect):
-    """Which patches' boxes rest on the proven allowance and which on round 1's empirical one: none of
-    cfg1/cfg2/cfg3's or the north-star lens's (cfg4), 126 of cfg5's 301 056."""
+def test_rounding_dominated_patches_are_always_tested(bzr, cfg_name, expect):
+    """Culling is exact by construction: a patch is in the tree only if its gate region is proven
+    (bvh.cpp: I - gamma_3 |M^-1| |M| a nonsingular M-matrix; build_bvh throws if a reachable leaf is not),
+    and the others -- none of cfg1/cfg2/cfg3's or the north-star lens's (cfg4), 126 rounding-dominated + 5
+    non-finite of cfg5's 301 056 -- form the always list every wave-segment gate-tests (both tiers, identical)."""
     patches = build_lens(bzr.TriMesh, CONFIGS[cfg_name].lenses[0]).bezier_patches()
-    assert len(rounding_dominated(patches)) == expect
+    dom = rounding_dominated(patches)
+    assert len(dom) == expect
+    # plus the records whose M is not finite (cfg5: 5 degenerate patches; they had the always-hit box before)
+    nonfinite = np.nonzero(~np.isfinite(patches[:, 49:58]).all(axis=1))[0]
+    assert len(nonfinite) == (5 if cfg_name == "cfg5" else 0)
+    want = np.union1d(dom, nonfinite).astype(np.uint32)
+    for tier in TIERS:
+        alw = always_list(bzr, patches, tier)
+        assert np.array_equal(alw, want), tier
+        if len(alw):  # their boxes are the always-hit box
+            boxes, _ = gate_boxes(bzr, patches, tier)
+            assert np.isinf(boxes[alw]).all()
+
+
+def test_always_list_in_traversal_replay(bzr):
+    """The host replay of the device walk reaches every always-listed patch for every active ray: 4000
+    of cfg5's patch records including its 131 unproven ones (the walk reads the records only)."""
+    full = build_lens(bzr.TriMesh, CONFIGS["cfg5"].lenses[0]).bezier_patches()
+    rng = np.random.default_rng(3)
+    pick = np.union1d(rng.choice(len(full), 4000, replace=False), np.union1d(
+        rounding_dominated(full), np.nonzero(~np.isfinite(full[:, 49:58]).all(axis=1))[0]))
+    patches = np.ascontiguousarray(full[pick])
+    alw = always_list(bzr, patches, 0)
+    assert len(alw) >= 131
+    rays = random_rays(rng, 256, (10.0, 0.0, 0.0), 3.0)
+    L = bzr.lib()
+    fn = L.bzr_debug_traverse
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32,
+                   ctypes.c_void_p, ctypes.c_void_p]
+    fn.restype = ctypes.c_int32
+    hits = np.zeros((rays.shape[1], len(patches)), np.uint8)
+    stats = np.zeros(4, np.uint64)
+    p = np.ascontiguousarray(patches, np.float32)
+    r = np.ascontiguousarray(rays)
+    assert fn(p.ctypes.data, len(p), 264, r.ctypes.data, r.shape[1], hits.ctypes.data, stats.ctypes.data) == 0
+    assert hits[:, alw].all()
 
 
 @pytest.mark.parametrize("cfg_name", ["cfg2", "cfg5"])

@@ -1,0 +1,82 @@
+"""Build-variant libraries (cuda-bezier-triangle-raytracer_amd/Makefile `variants`, built by build()).
+
+stack4: libbzr with a 4-entry traversal stack (-DBZR_STACK=4).  Lanes whose walk runs out of stack
+mid-walk switch to the reference's in-order full scan (reference/bezierMesh.cpp:206-227) while keeping
+what the walk already found -- duplicates must collapse under the (t, scanned index) key and parked /
+joined retry state must stay valid across the switch.  The default 64-entry stack never overflows on the
+bench configs, so only this build exercises that path: fused == staged == brute force (and == the oracle
+on cfg2), bit for bit, with the device counters reporting overflow rays.
+
+The variant runs in a child process (BZR_LIBRARY selects the library; one process = one libbzr).
+"""
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+REPO = Path(__file__).resolve().parents[1]
+PKG = REPO / "cuda-bezier-triangle-raytracer_amd"
+
+WORKER = r"""
+import json, sys
+import numpy as np
+sys.path[:0] = [sys.argv[1], sys.argv[2]]
+import bzr_amd as bzr
+from bzr_amd.configs import CONFIGS, build_lens, grid_rays, pixel_coords, rays_for
+from oracle import pyoracle as orc
+
+def bits(a):
+    return np.ascontiguousarray(a).view(np.uint32)
+
+ctx = bzr.Context(0)
+out = {}
+# cfg2: one lens, the refraction chain, 256^2 primaries (oracle too)
+lens = build_lens(bzr.TriMesh, CONFIGS["cfg2"].lenses[0]).bezier_patches()
+dm = bzr.DeviceMesh(ctx, lens)
+rays = grid_rays(CONFIGS["cfg2"], side=256)
+want = orc.trace_chain([lens], [1.3], rays)
+for name, mode in (("fused", bzr.PIPELINE_FUSED), ("staged", bzr.PIPELINE_STAGED), ("brute", bzr.ACCEL_NONE)):
+    ctx.counters(True); ctx.counters_report()
+    got = bzr.trace_chain(ctx, [dm], [1.3], rays, mode=mode)
+    c = ctx.counters_report(); ctx.counters(False)
+    out[f"cfg2_{name}_equal"] = all(np.array_equal(bits(g), bits(w)) for g, w in zip(got, want))
+    out[f"cfg2_{name}_overflow_rays"] = c["overflow_rays"]
+# cfg5: 301 056 patches, BezierMesh::intersect on 65 536 grid rays from the lens's middle rows
+cfg = CONFIGS["cfg5"]
+p5 = build_lens(bzr.TriMesh, cfg.lenses[0]).bezier_patches()
+dm5 = bzr.DeviceMesh(ctx, p5)
+r, c = pixel_coords(cfg, side=8192, order="tiles")
+mid = len(r) // 2
+rays5 = rays_for(cfg, r[mid:mid + 65536], c[mid:mid + 65536], side=8192)
+ref = bits(bzr.intersect(ctx, dm5, rays5, mode=bzr.ACCEL_NONE))
+out["cfg5_hits"] = int((ref[11] == 4).sum())
+for name, mode in (("fused", bzr.PIPELINE_FUSED), ("staged", bzr.PIPELINE_STAGED)):
+    ctx.counters(True); ctx.counters_report()
+    got = bits(bzr.intersect(ctx, dm5, rays5, mode=mode))
+    cnt = ctx.counters_report(); ctx.counters(False)
+    out[f"cfg5_{name}_equal"] = bool(np.array_equal(got, ref))
+    out[f"cfg5_{name}_overflow_rays"] = cnt["overflow_rays"]
+print(json.dumps(out))
+"""
+
+
+@pytest.mark.gpu
+def test_tiny_stack_overflow_path_is_exact():
+    lib = PKG / "lib" / "stack4" / "libbzr.so"
+    if not lib.exists():
+        pytest.fail(f"{lib} missing: build() makes the `variants` target")
+    env = dict(os.environ, BZR_LIBRARY=str(lib))
+    res = subprocess.run([sys.executable, "-c", WORKER, str(PKG), str(REPO)], env=env, capture_output=True,
+                         text=True, timeout=110)
+    assert res.returncode == 0, res.stderr[-2000:]
+    out = json.loads(res.stdout.strip().splitlines()[-1])
+    for k, v in out.items():
+        if k.endswith("_equal"):
+            assert v, (k, out)
+    # the tiny stack really overflowed on both pipelines (the brute-force scan has no stack)
+    for k in ("cfg2_fused", "cfg2_staged", "cfg5_fused", "cfg5_staged"):
+        assert out[f"{k}_overflow_rays"] > 0, (k, out)
+    assert out["cfg5_hits"] > 10000
