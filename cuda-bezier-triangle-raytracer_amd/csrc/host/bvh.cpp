@@ -604,6 +604,81 @@ uint32_t collapse(std::vector<BvhNode> const &bin, uint32_t n2, std::vector<Bvh4
   return id;
 }
 
+// Wedge pre-test of an always-listed patch (8 floats: w.xyz, L, H, B, C, 0; Bvh::always_wedge).  No box
+// bounds where its float gate passes, but a slab does once |p| is known: for any direction w and
+// g = M^-T w (so M^T g = w + r), a passing float plane point p has y = M p with y_k = b_k - e_k, b_k in
+// [0,1], |e_k| <= gamma_3 |M_k|_1 |p|_inf, hence
+//   w.p = g.y - r.p  in  [L - B |p|_inf, H + B |p|_inf],  L = sum min(0, g_k), H = sum max(0, g_k),
+//   B = gamma_3 sum_k |g_k| |M_k|_1 + |r|_1.
+// w = M's middle right singular vector (eigenvector of M^T M) makes the slab a thin in-plane wedge
+// around M's near-null direction (the one the gate's rounding noise runs along): on cfg5 it rejects ~97 %
+// of (ray, patch) pairs before the division.  The device evaluates w.p~ at p~ = s + d (num x rcp(cs)),
+// within 14 u (|s| + |p~|) of the gate's own p (inf-norm; u = 2^-24; plane_ray's rounding plus v_rcp_f32's
+// 1 ulp), so it widens both sides by C (|s| + |p~|), C = 32 u + 14 u B (also covering its own dot
+// product).  Any direction is valid, so the eigenvector's accuracy only affects tightness; g's is
+// covered by the residual r.  Open wedge (L = -inf, H = +inf) when M or its inverse is not finite.
+void always_wedge(const float *rec, float out[8]) {
+  out[0] = out[1] = out[2] = 0.0f;
+  out[3] = -HUGE_VALF;
+  out[4] = HUGE_VALF;
+  out[5] = out[6] = out[7] = 0.0f;
+  const float *m = rec + 49;  // col-major
+  double M[3][3];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) M[i][j] = m[j * 3 + i];
+  for (auto const &r : M)
+    for (double x : r)
+      if (!std::isfinite(x)) return;
+  double det = M[0][0] * (M[1][1] * M[2][2] - M[1][2] * M[2][1]) - M[0][1] * (M[1][0] * M[2][2] - M[1][2] * M[2][0]) +
+               M[0][2] * (M[1][0] * M[2][1] - M[1][1] * M[2][0]);
+  if (!(std::fabs(det) > 0) || !std::isfinite(det)) return;
+  double Q[3][3];  // M^-1 by cofactors
+  for (int i = 0; i < 3; ++i)
+    for (int k = 0; k < 3; ++k) {
+      const int r1 = (k + 1) % 3, r2 = (k + 2) % 3, c1 = (i + 1) % 3, c2 = (i + 2) % 3;
+      Q[i][k] = (M[r1][c1] * M[r2][c2] - M[r1][c2] * M[r2][c1]) / det;
+    }
+  double A[3][3], V[3][3];  // M^T M and its eigenvectors (columns, decreasing eigenvalue)
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) A[i][j] = M[0][i] * M[0][j] + M[1][i] * M[1][j] + M[2][i] * M[2][j];
+  eigen_sym3(A, V);
+  double w[3] = {V[0][1], V[1][1], V[2][1]};
+  const double wn = std::sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+  if (!(wn > 0)) return;
+  for (double &x : w) x = static_cast<float>(x / wn);  // the float direction the device uses, exactly
+  double g[3];  // g = Q^T w
+  for (int k = 0; k < 3; ++k) g[k] = Q[0][k] * w[0] + Q[1][k] * w[1] + Q[2][k] * w[2];
+  double r1 = 0.0, gm = 0.0;  // |M^T g - w|_1, and a scale for the double rounding of that residual
+  for (int l = 0; l < 3; ++l) {
+    double acc = -w[l], mag = std::fabs(w[l]);
+    for (int k = 0; k < 3; ++k) {
+      acc += M[k][l] * g[k];
+      mag += std::fabs(M[k][l] * g[k]);
+    }
+    r1 += std::fabs(acc);
+    gm = std::max(gm, mag);
+  }
+  const double g3 = 3.0000002 / 16777216.0, u = 1.0 / 16777216.0;
+  double L = 0.0, H = 0.0, B = r1 + 1e-12 * gm;
+  for (int k = 0; k < 3; ++k) {
+    L += std::min(0.0, g[k]);
+    H += std::max(0.0, g[k]);
+    B += g3 * std::fabs(g[k]) * (std::fabs(M[k][0]) + std::fabs(M[k][1]) + std::fabs(M[k][2]));
+  }
+  L -= 1e-9 * (std::fabs(L) + 1.0);
+  H += 1e-9 * (std::fabs(H) + 1.0);
+  B = B * (1.0 + 1e-9) + 1e-30;
+  const double C = 32.0 * u + 14.0 * u * B;
+  if (!std::isfinite(L) || !std::isfinite(H) || !std::isfinite(B)) return;
+  out[0] = static_cast<float>(w[0]);
+  out[1] = static_cast<float>(w[1]);
+  out[2] = static_cast<float>(w[2]);
+  out[3] = std::nextafter(static_cast<float>(L), -HUGE_VALF);
+  out[4] = std::nextafter(static_cast<float>(H), HUGE_VALF);
+  out[5] = std::nextafter(static_cast<float>(B), HUGE_VALF);
+  out[6] = std::nextafter(static_cast<float>(C), HUGE_VALF);
+}
+
 }  // namespace
 
 // Patches whose gate-region box exceeds kWideRatio x their triangle's extent go to the wide subtree
@@ -643,6 +718,10 @@ Bvh build_bvh(const float *records, uint32_t n, uint32_t stride_words, int tier)
   {
     auto mid = std::stable_partition(out.order.begin(), out.order.end(), [&](uint32_t i) { return region[i].proven; });
     out.always.assign(mid, out.order.end());
+    std::sort(out.always.begin(), out.always.end());
+    out.always_wedge.assign(out.always.size() * 8, 0.0f);
+    for (size_t k = 0; k < out.always.size(); ++k)
+      always_wedge(records + (size_t)out.always[k] * stride_words, &out.always_wedge[8 * k]);
   }
   const uint32_t n_tree = n - static_cast<uint32_t>(out.always.size());
   // Wide patches: gate regions much larger than their own triangle (planes through or near the
@@ -932,6 +1011,15 @@ extern "C" int32_t bzr_debug_always_list(const void *patches, uint32_t n, uint32
   bzr_host::Bvh bvh = bzr_host::build_bvh(static_cast<const float *>(patches), n, stride / 4, tier);
   *count = static_cast<uint32_t>(bvh.always.size());
   if (out) std::memcpy(out, bvh.always.data(), bvh.always.size() * sizeof(uint32_t));
+  return 0;
+}
+
+// The always list's wedge pre-test words (bvh.hpp Bvh::always_wedge), 8 floats per always-listed patch.
+extern "C" int32_t bzr_debug_always_wedges(const void *patches, uint32_t n, uint32_t stride, int32_t tier, float *out) {
+  if ((!patches && n) || !out || stride % 4 || stride < 264) return 1;
+  if (tier != bzr_host::kTierFar && tier != bzr_host::kTierNear) return 1;
+  bzr_host::Bvh bvh = bzr_host::build_bvh(static_cast<const float *>(patches), n, stride / 4, tier);
+  std::memcpy(out, bvh.always_wedge.data(), bvh.always_wedge.size() * sizeof(float));
   return 0;
 }
 

@@ -58,6 +58,10 @@ struct Bvh {
                                    // are [0, n - always.size()), the always-tested patches follow
   std::vector<uint32_t> always;    // patches whose gate region has no proven bound (bvh.cpp), ascending:
                                    // not in the tree, every wave-segment gate-tests them
+  std::vector<float> always_wedge; // per always patch, 8 floats: w.xyz, L, H, B, C, 0 -- the in-plane wedge a
+                                   // passing float plane point p lies in, L - B|p| - C(|s|+|p|) <= w.p <=
+                                   // H + B|p| + C(|s|+|p|) (inf-norms; bvh.cpp always_wedge): a proven
+                                   // pre-test that skips most always-list gates
   std::vector<float> patch_box;    // per order slot: lo.xyz, 0, hi.xyz, 0 (the gate-region box)
   float extent = 0.0f;             // max |coordinate| of any finite box
   float s_max = 0.0f;              // rays with |origin|_inf > s_max take the brute-force path

@@ -20,6 +20,10 @@ int32_t bzr_debug_gate_boxes_tier(const void *patches, uint32_t n, uint32_t stri
  * Returns 0 on success. */
 int32_t bzr_debug_always_list(const void *patches, uint32_t n, uint32_t stride, int32_t tier, uint32_t *out,
                               uint32_t *count);
+/* The always list's wedge pre-test (bvh.cpp always_wedge), 8 floats per always-listed patch in list order:
+ * w.xyz, L, H, B, C, 0.  A lane whose float plane point p~ = s + d (num x rcp(cs)) has w.p~ outside
+ * [L - B|p~| - C(|s|+|p~|), H + B|p~| + C(|s|+|p~|)] cannot pass that patch's gate. */
+int32_t bzr_debug_always_wedges(const void *patches, uint32_t n, uint32_t stride, int32_t tier, float *out);
 /* The oriented gate-region boxes of one tier's wide-patch subtree (bvh.hpp Bvh4ObbNode), by patch index:
  * out[16*i] = centre xyz, axes u v w (xyz each), half extents (3), then 1.0f if patch i is a wide patch
  * (its parent node tests this box) or 0.0f (16 zeros: the patch is AABB-culled).  Returns 0 on success. */

@@ -349,3 +349,81 @@ def test_plane_point_rounding_within_derived_bounds(bzr, cfg_name):
     line = np.linalg.norm(w - (w * d64).sum(1, keepdims=True) * d64 / (d64 * d64).sum(1, keepdims=True), axis=1)
     assert (off <= 16 * scale).all(), (off / scale).max()
     assert (line <= 2 * np.sqrt(3) * scale).all(), (line / scale).max()
+
+
+def always_wedges(bzr, patches, tier, count):
+    L = bzr.lib()
+    fn = L.bzr_debug_always_wedges
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int32, ctypes.c_void_p]
+    fn.restype = ctypes.c_int32
+    p = np.ascontiguousarray(patches, np.float32)
+    out = np.zeros((count, 8), np.float32)
+    assert fn(p.ctypes.data, len(p), 264, tier, out.ctypes.data) == 0
+    return out
+
+
+def wedge_keep_f32(patches, wedges, rays):
+    """float32 replica of trace.hip always_gate's two pre-tests: keep[r, k] unless the lane surely fails
+    (fma steps rounded once via float64; 1/x where the device uses v_rcp_f32, which the C term covers)."""
+    f = np.float32
+    s = rays[:3].T.astype(f)[:, None, :]
+    d = rays[3:].T.astype(f)[:, None, :]
+    n, c = patches[None, :, 0:3].astype(f), patches[None, :, 3].astype(f)
+
+    def dot(a, b):
+        return (a[..., 0] * b[..., 0] + (a[..., 1] * b[..., 1] + a[..., 2] * b[..., 2])).astype(f)
+
+    with np.errstate(all="ignore"):
+        cs = dot(d, n)
+        num = (c - dot(n, s)).astype(f)
+        keep = (np.abs(cs) >= f(1e-5)) & (((num > 0) & (cs > 0)) | ((num < 0) & (cs < 0)))
+        keep |= np.isnan(num) | np.isnan(cs)
+        tt = (num * (f(1) / cs)).astype(f)
+        p = (d.astype(np.float64) * tt[..., None] + s.astype(np.float64)).astype(f)
+        pm, sm = np.abs(p).max(-1), np.abs(s).max(-1)
+        w = wedges[None, :, :3].astype(np.float64)
+        z = (w[..., 2] * p[..., 2]).astype(f).astype(np.float64)
+        y = (w[..., 1] * p[..., 1] + z).astype(f).astype(np.float64)
+        wd = (w[..., 0] * p[..., 0] + y).astype(f)
+        slack = (wedges[None, :, 5].astype(np.float64) * pm + (wedges[None, :, 6] * (sm + pm)).astype(f)).astype(f)
+        hi = (wedges[None, :, 4] + slack).astype(f)
+        lo = (wedges[None, :, 3] - slack).astype(f)
+        keep &= ~(wd > hi) & ~(wd < lo)
+    return keep
+
+
+@pytest.mark.slow
+def test_always_wedge_keeps_every_gate_pass(bzr, orc):
+    """The always list's wedge pre-test (bvh.cpp always_wedge, trace.hip always_gate) may only reject lanes
+    whose planar gate fails: every gate pass of cfg5's always-listed patches -- config rays and rays aimed
+    at those patches from near the origin -- is kept, and most pairs are rejected (the point of it)."""
+    cfg = CONFIGS["cfg5"]
+    patches = build_lens(bzr.TriMesh, cfg.lenses[0]).bezier_patches()
+    alw = always_list(bzr, patches, 0)
+    wed = always_wedges(bzr, patches, 0, len(alw))
+    assert np.array_equal(wed, always_wedges(bzr, patches, 1, len(alw)))
+    pa = patches[alw]
+    fin = np.isfinite(pa[:, 49:58]).all(axis=1)
+    assert (np.isinf(wed[~fin, 3]) & np.isinf(wed[~fin, 4])).all()  # non-finite records: open wedge
+    rng = np.random.default_rng(29)
+    from bzr_amd.configs import pixel_coords, rays_for
+    r, c = pixel_coords(cfg, side=8192, order="rows")
+    pick = rng.choice(len(r), 60000, replace=False)
+    sets = [rays_for(cfg, r[pick], c[pick], side=8192)]
+    for m, jitter, spread in ((40000, 0.05, 6.0), (40000, 0.5, 20.0)):
+        o = rng.uniform(-spread, spread, (m, 3))
+        tgt = pa[fin][rng.integers(0, fin.sum(), m), 19:22] + rng.normal(size=(m, 3)) * jitter
+        d = tgt - o
+        d /= np.linalg.norm(d, axis=1, keepdims=True)
+        sets.append(np.concatenate([o.T, d.T]).astype(np.float32))
+    passes = kept = total = 0
+    for k, rays in enumerate(sets):
+        gate = orc.planar_gate(pa, rays, threads=8)
+        keep = wedge_keep_f32(pa, wed, rays)
+        missed = gate & ~keep
+        assert not missed.any(), f"set {k}: {int(missed.sum())} gate passes rejected, e.g. {np.argwhere(missed)[:4]}"
+        passes += int(gate.sum())
+        if k == 0:
+            kept, total = int(keep.sum()), keep.size
+    assert passes > 100
+    assert kept < 0.1 * total  # the config rays: most (ray, always patch) pairs never reach the gate
