@@ -63,8 +63,8 @@ def parse():
     p.add_argument("--config", default="cfg4", choices=["cfg2", "cfg3", "cfg4", "cfg5"])
     p.add_argument("--side", type=int, default=0, help="override rays per image side")
     p.add_argument("--scaling", default="strong", choices=["strong", "weak"])
-    p.add_argument("--gather", default="image", choices=["image", "rays", "none"],
-                   help="what each frame sends to rank 0 when N > 1 (DESIGN.md (e) byte budget)")
+    p.add_argument("--gather", default="image", choices=["image", "rays", "compact", "none"],
+                   help="what each frame sends to rank 0 when N > 1 (frame.py layouts, DESIGN.md (e) byte budget)")
     p.add_argument("--accel", default="bvh", choices=["bvh", "none"], help="none = brute-force scan (A/B)")
     p.add_argument("--pipeline", default="fused", choices=["fused", "staged", "auto"],
                    help="culled-path pipeline (include/bzr.h BZR_PIPELINE_*; same output bits): fused = one k_trace "
@@ -245,57 +245,20 @@ def main():
         outs = [torch.empty((13, n), dtype=torch.float32, device=dev) for _ in range(F)]
         hits = outs[0]
     gather = world > 1 and a.gather != "none"
-    # rays layout: the whole result (chain: 6 ray rows + status/segment word; intersect: the 13 hit rows);
-    # image layout: one word per primary (chain: status | segments << 8; intersect: the hit's `what` row)
-    rows = 1 if a.gather == "image" else (frame.PACKED_ROWS if chain else 13)
-    # double-buffered frame gather: frame k's packed results travel to rank 0 (RCCL, its own stream)
-    # while frame k+1 is traced; a buffer is refilled only after its previous gather completed.  Buffers
-    # hold the largest rank's share (strong scaling may deal one tile fewer to some ranks).
     npad = frame.padded_count(world, side, height)
-    packed = [torch.zeros((rows, npad), dtype=torch.float32, device=dev) for _ in range(2)] if gather else None
-    gather_lists = [[torch.empty_like(packed[0]) for _ in range(world)] if (gather and rank == 0) else None
-                    for _ in range(2)]
-    pending = [None, None]
-    frames = [0]
 
-    def step(inflight=F):
-        f = frames[0] % inflight  # frame slot: context, stream, outputs
-        with torch.cuda.stream(streams[f]):
-            if chain:
-                bzr_amd.trace_chain(ctxs[f], meshes, ris, rays, *outs[f], mode=mode)
-            else:
-                bzr_amd.intersect(ctxs[f], meshes[0], rays, outs[f], mode=mode)
-            if gather:
-                slot = frames[0] % 2
-                if pending[slot] is not None:
-                    pending[slot].wait()
-                if chain:
-                    frame.pack(*outs[f], packed[slot])
-                elif rows == 1:
-                    packed[slot][0, :n].copy_(outs[f][11])
-                else:
-                    packed[slot][:, :n].copy_(outs[f])
-                pending[slot] = frame.gather(packed[slot], world, rank, gather_list=gather_lists[slot], async_op=True)
-        frames[0] += 1
-
-    def join_streams():  # stream 0 waits for the other slots' queued frames
-        for st in streams[1:]:
-            ev = torch.cuda.Event()
-            ev.record(st)
-            streams[0].wait_event(ev)
-
-    def drain():
-        for k in range(2):
-            if pending[k] is not None:
-                pending[k].wait()
-                pending[k] = None
+    def trace(f, k):  # frame k on slot f: its context, stream (the loop's stream_for) and outputs
+        if chain:
+            bzr_amd.trace_chain(ctxs[f], meshes, ris, rays, *outs[f], mode=mode)
+        else:
+            bzr_amd.intersect(ctxs[f], meshes[0], rays, outs[f], mode=mode)
 
     # work counters of one frame (device-side; measured here, outside the timed region)
     ctx.counters(True)
     ctx.counters_report()
-    frames[0] = 0
-    step(inflight=1)
-    drain()
+    with torch.cuda.stream(streams[0]):
+        trace(0, 0)
+    torch.cuda.synchronize()
     work_cnt = ctx.counters_report()
     ctx.counters(False)
     seg_local = int(out_seg.sum().item()) if chain else n
@@ -303,6 +266,39 @@ def main():
     if world > 1:
         dist.all_reduce(seg_total)
     seg_total = int(seg_total.item())
+    # compact gather (frame.py): survivor capacity from this frame's largest rank share
+    cap = 0
+    if a.gather == "compact":
+        if not chain:
+            raise SystemExit("--gather compact applies to the refraction-chain configs (cfg2, cfg4)")
+        cnt = frame.survivors(out_status, out_seg).sum().reshape(1).to(torch.int64)
+        if world > 1:
+            dist.all_reduce(cnt, op=dist.ReduceOp.MAX)
+        cap = frame.compact_capacity(int(cnt.item()), npad)
+    # The frame loop (frame.FrameLoop): frames in flight, and with N > 1 a double-buffered asynchronous gather
+    # -- frame k's packed results travel to rank 0 (RCCL, its own stream) while frame k+1 is traced; a
+    # buffer is refilled only after its previous gather completed.  Buffers hold the largest rank's share
+    # (strong scaling may deal one tile fewer to some ranks).  Layouts: rays (chain: 6 ray rows + the
+    # status/segment word; intersect: the 13 hit rows), compact (every final ray, survivors only), image
+    # (one word per primary; intersect: the hit's `what` row).
+    pack_fn = None
+    if not chain:
+        pack_fn = ((lambda out, p: p[0, :n].copy_(out[11])) if a.gather == "image" else
+                   (lambda out, p: p[:, :n].copy_(out)))
+    loop = frame.FrameLoop(world, rank, n, npad, a.gather, trace, outs, stream_for=lambda f: torch.cuda.stream(streams[f]),
+                           cap=cap, device=dev, pack_fn=pack_fn, rows=0 if chain else 13)
+
+    def step(inflight=F):
+        loop.step(inflight)
+
+    def join_streams():  # stream 0 waits for the other slots' queued frames
+        for st in streams[1:]:
+            ev = torch.cuda.Event()
+            ev.record(st)
+            streams[0].wait_event(ev)
+
+    drain = loop.drain
+
     # the W warmup steps run right before the timed ones (no host round trip in between)
     for _ in range(a.warmup):
         step()
@@ -401,8 +397,11 @@ def main():
                 "segments_per_step": seg_total,
                 "patches": n_patch,
                 "parallelism": f"64x64 image tiles round-robin over {world} rank(s), {a.scaling} scaling"
-                               + (f", RCCL gather of every frame to rank 0 (overlapped with the next frame): "
-                                  f"{rows * 4} B per primary ({a.gather})" if gather else ""),
+                               + (f", RCCL gather of every frame to rank 0 (overlapped with the next frames): "
+                                  f"{loop.bytes_per_rank / npad:.2f} B per primary ({a.gather})" if gather else ""),
+                "gather": ({"layout": a.gather, "bytes_per_rank_per_frame": loop.bytes_per_rank,
+                            "bytes_per_primary": round(loop.bytes_per_rank / npad, 3), "compact_capacity": cap or None}
+                           if gather else None),
                 "pipeline": a.pipeline,
                 "frames_in_flight": F,
                 "hw_queues": {"GPU_MAX_HW_QUEUES": hwq, "source": _HWQ_SOURCE,

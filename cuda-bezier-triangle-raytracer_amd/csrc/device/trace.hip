@@ -1547,10 +1547,12 @@ bzr_status check_ctx_mesh(bzr_ctx *ctx, const bzr_mesh *mesh) {
 bool use_scan(uint32_t flags) { return (flags & BZR_ACCEL_NONE) != 0; }
 bool use_fast(uint32_t flags) { return (flags & BZR_MODE_FAST) != 0; }
 // Culled-path pipeline for a call of n rays over meshes of at most nb patches (include/bzr.h): forced by
-// BZR_PIPELINE_STAGED / BZR_PIPELINE_FUSED, otherwise fused for dense batches (rays per patch >= 2048:
-// cfg4 at 4096^2 has 5461 and a wave's 64 rays meet ~2 patches per segment, fused 1.2x faster; cfg2 at
-// 1024^2 has 341 and staged is 1.5x faster there; cfg5 has 56-223, staged 1.3x), DESIGN.md (a).
-constexpr uint64_t kFusedRaysPerPatch = 2048;
+// BZR_PIPELINE_STAGED / BZR_PIPELINE_FUSED, otherwise fused for dense batches (rays per patch >= 256;
+// rays per patch stands in for how many patches a wave's 64 rays meet).  Chosen for callers that keep
+// frames in flight (bench.py): cfg4 at 4096^2 (5461 rays per patch) and cfg2 at 1024^2
+// (341) run fused -- cfg2 5593 vs 5205 Mrays/s at three / two frames in flight, though a lone cfg2 frame
+// is faster staged; cfg3 (145) and cfg5 (223) run staged.
+constexpr uint64_t kFusedRaysPerPatch = 256;
 bool use_staged(uint32_t flags, uint64_t n, uint64_t nb) {
   if (flags & BZR_PIPELINE_STAGED) return true;
   if (flags & BZR_PIPELINE_FUSED) return false;

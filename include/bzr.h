@@ -76,7 +76,7 @@ enum {
    *           few distinct patches (dense ray grids: more than ~2000 rays per patch)
    *   staged  traverse -> bucket pairs by patch -> Newton -> resolve -> finish per segment; full-wave
    *           Newton passes whatever the ray coherence, at ~12x the algorithmic HBM bytes
-   * automatic: fused when n >= 2048 x the largest lens's patch count, else staged. */
+   * automatic: fused when n >= 256 x the largest lens's patch count, else staged. */
   BZR_PIPELINE_STAGED = 8u,
   BZR_PIPELINE_FUSED = 16u
 };

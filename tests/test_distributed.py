@@ -100,3 +100,93 @@ def test_tile_deal_covers_the_image_centre_first(world):
         w = rows.reshape(-1, 64)  # one wavefront: an 8x8 block
         assert np.all(w.max(axis=1) - w.min(axis=1) == 7)
     assert np.all(seen == 1)
+
+
+def loop_worker(rank, world, port, width, height, patches, result_path, layout, inflight, frames):
+    """bench.py's loop (frame.FrameLoop): `inflight` slots, double-buffered async gather, the oracle as
+    each slot's tracer; frame k refracts with ri = 1.3 + 0.02 k so every frame's result differs and a
+    frame gathered under the wrong index would be caught.  Rank 0 assembles every frame as it lands."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import pyoracle
+
+        cfg = CONFIGS["cfg2"]
+        rows, cols, rays = frame.rank_rays(cfg, rank, world, width, height)
+        n = rays.shape[1]
+        npad = frame.padded_count(world, width, height)
+        outs = [(torch.zeros((6, n)), torch.zeros(n, dtype=torch.int32), torch.zeros(n, dtype=torch.int32))
+                for _ in range(inflight)]
+
+        def trace(slot, k):
+            o, s, g = pyoracle.trace_chain([patches], [1.3 + 0.02 * k], rays, threads=2)
+            outs[slot][0].copy_(torch.from_numpy(o))
+            outs[slot][1].copy_(torch.from_numpy(s.view(np.int32)))
+            outs[slot][2].copy_(torch.from_numpy(g.view(np.int32)))
+
+        cap = 0
+        if layout == "compact":  # capacity from a first frame's survivor count (max over ranks), as bench.py
+            trace(0, 0)
+            cnt = torch.tensor([int(frame.survivors(outs[0][1], outs[0][2]).sum())])
+            dist.all_reduce(cnt, op=dist.ReduceOp.MAX)
+            cap = frame.compact_capacity(int(cnt[0]), npad)
+        got = {}
+
+        def on_gathered(k, parts):
+            got[k] = frame.assemble(parts, cfg, world, width, height, cap=cap)
+
+        loop = frame.FrameLoop(world, rank, n, npad, layout, trace, outs, cap=cap, on_gathered=on_gathered)
+        for _ in range(frames):
+            loop.step(inflight)
+        loop.drain()
+        if rank == 0:
+            np.savez(result_path, **{f"{name}{k}": a for k, v in got.items() for name, a in zip(("rays", "status", "seg"), v)
+                                     if a is not None}, frames=np.array(sorted(got)), bytes=np.array(loop.bytes_per_rank))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("layout", ["compact", "rays", "image"])
+def test_frame_loop_inflight_async_gather(bzr, orc, tmp_path, layout):
+    """frame.FrameLoop at world size 2 with 3 frames in flight and 5 frames: every frame lands on rank 0
+    once, under its own index, equal to a single-process trace of that frame; the compact layout delivers
+    every final ray in fewer bytes than the rays layout."""
+    cfg = CONFIGS["cfg2"]
+    patches = bzr.TriMesh().make_ellipsoid(32, 16, (1, 4, 2)).translate((10, 0, 0)).standardize().bezier_patches()
+    width = height = 128
+    world, inflight, frames = 2, 3, 5
+    out = tmp_path / "loop.npz"
+    mp.start_processes(loop_worker, args=(world, free_port(), width, height, patches, str(out), layout, inflight, frames),
+                       nprocs=world, join=True, start_method="spawn")
+    got = np.load(out)
+    assert list(got["frames"]) == list(range(frames))
+    rows, cols, rays = frame.rank_rays(cfg, 0, 1, width, height)
+    flat = rows * width + cols
+    for k in range(frames):
+        o, s, g = orc.trace_chain([patches], [1.3 + 0.02 * k], rays)
+        assert np.array_equal(got[f"status{k}"][flat], s) and np.array_equal(got[f"seg{k}"][flat], g), k
+        if layout != "image":
+            assert np.array_equal(got[f"rays{k}"][:, flat].view(np.uint32), o.view(np.uint32)), k
+    npad = frame.padded_count(world, width, height)
+    if layout == "compact":
+        assert int(got["bytes"]) < 0.8 * frame.PACKED_ROWS * 4 * npad
+
+
+def test_compact_capacity_overflow_is_reported():
+    """A frame with more survivors than the compact capacity is refused on rank 0, not truncated."""
+    n = npad = 4096
+    status = torch.zeros(n, dtype=torch.int32)
+    seg = torch.full((n,), 2, dtype=torch.int32)
+    seg[:100] = 1
+    rays = torch.randn(6, n)
+    cap = 1000
+    packed = torch.zeros(frame.compact_size(npad, cap))
+    frame.pack_compact(status, seg, rays, packed, npad, cap)
+    with pytest.raises(RuntimeError, match="capacity"):
+        frame.unpack_compact(packed, n, npad, cap, np.zeros((6, n), np.float32))
+    cap = n
+    packed = torch.zeros(frame.compact_size(npad, cap))
+    frame.pack_compact(status, seg, rays, packed, npad, cap)
+    r, st, sg = frame.unpack_compact(packed, n, npad, cap, np.zeros((6, n), np.float32))
+    assert np.array_equal(r[:, 100:], rays.numpy()[:, 100:]) and (r[:, :100] == 0).all()
+    assert np.array_equal(sg, seg.numpy().astype(np.uint32))

@@ -51,6 +51,12 @@ dm5 = bzr.DeviceMesh(ctx, p5)
 r, c = pixel_coords(cfg, side=8192, order="tiles")
 mid = len(r) // 2
 rays5 = rays_for(cfg, r[mid:mid + 65536], c[mid:mid + 65536], side=8192)
+# plus incoherent rays from all around the lens (deep, diverging walks: the ones that overflow a tiny stack)
+rng = np.random.default_rng(41)
+o = rng.uniform(-12, 12, (16384, 3)) + np.array([10.0, 0.0, 0.0])
+tgt = np.array([10.0, 0.0, 0.0]) + rng.uniform(-1, 1, (16384, 3)) * np.array([1.0, 4.0, 2.0])
+dd = (tgt - o) / np.linalg.norm(tgt - o, axis=1, keepdims=True)
+rays5 = np.concatenate([rays5, np.concatenate([o.T, dd.T]).astype(np.float32)], axis=1)
 ref = bits(bzr.intersect(ctx, dm5, rays5, mode=bzr.ACCEL_NONE))
 out["cfg5_hits"] = int((ref[11] == 4).sum())
 for name, mode in (("fused", bzr.PIPELINE_FUSED), ("staged", bzr.PIPELINE_STAGED)):
