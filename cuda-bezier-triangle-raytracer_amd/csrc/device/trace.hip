@@ -545,6 +545,99 @@ __device__ __forceinline__ bool always_gate(const float4 *always, uint32_t k, bo
   return keep & planar_gate(q0, leaf_q(r, 1), leaf_q(r, 2), leaf_q(r, 3), s, d);
 }
 
+// Wave-level pre-test of the always list.  The active rays of a wave form a bundle: origins in the box
+// [slo, shi], directions in [dlo, dhi] (wave min / max, once per segment).  Lane j tests always-listed
+// patch 64 b + j against the whole bundle in interval arithmetic: the ranges of cs = n.d and num = c - n.s
+// over the bundle (widened for the lanes' own float dot products), the plane distance t = num / cs over
+// the corners (t > 0 and |cs| >= 1e-5 needed), the plane points P = S + D T, and the wedge of
+// always_gate: w.P against [L - B|P| - ..., H + ...].  A patch whose interval misses is gate-failed by every
+// ray of the wave; only the survivors (a ballot mask, one bit per patch) take the per-lane tests -- 64
+// patches per VALU instruction instead of one.  Every margin rounds outward (u = 2^-24): the lanes' dot
+// products 8u, the corner quotients 6u, the points 8u, the wedge product and the bound 64u of (|S| + |P|).
+// Non-finite bundles (or t ranges beyond 1e30) keep everything.
+struct Bundle {
+  f3 slo, shi, dlo, dhi;
+  bool finite;
+};
+__device__ __forceinline__ float wave_minf(float v) {
+#pragma unroll
+  for (int k = 32; k >= 1; k >>= 1) v = fminf(v, __shfl_xor(v, k, 64));
+  return v;
+}
+__device__ __forceinline__ float wave_maxf(float v) {
+#pragma unroll
+  for (int k = 32; k >= 1; k >>= 1) v = fmaxf(v, __shfl_xor(v, k, 64));
+  return v;
+}
+__device__ __forceinline__ Bundle make_bundle(bool act, f3 s, f3 d) {
+  const float inf = __builtin_inff();
+  Bundle b;
+  b.slo = mk(wave_minf(act ? s.x : inf), wave_minf(act ? s.y : inf), wave_minf(act ? s.z : inf));
+  b.shi = mk(wave_maxf(act ? s.x : -inf), wave_maxf(act ? s.y : -inf), wave_maxf(act ? s.z : -inf));
+  b.dlo = mk(wave_minf(act ? d.x : inf), wave_minf(act ? d.y : inf), wave_minf(act ? d.z : inf));
+  b.dhi = mk(wave_maxf(act ? d.x : -inf), wave_maxf(act ? d.y : -inf), wave_maxf(act ? d.z : -inf));
+  const float m = fmaxf(fmaxf(fmaxf(fabsf(b.slo.x), fabsf(b.slo.y)), fmaxf(fabsf(b.slo.z), fabsf(b.shi.x))),
+                        fmaxf(fmaxf(fabsf(b.shi.y), fabsf(b.shi.z)),
+                              fmaxf(fmaxf(fabsf(b.dlo.x), fabsf(b.dlo.y)), fmaxf(fmaxf(fabsf(b.dlo.z), fabsf(b.dhi.x)),
+                                                                               fmaxf(fabsf(b.dhi.y), fabsf(b.dhi.z))))));
+  b.finite = m <= 1e30f;  // also false for an empty bundle (every box +-inf)
+  return b;
+}
+// Interval of n.x over x in [lo, hi] (n fixed).
+__device__ __forceinline__ void ivdot(f3 n, f3 lo, f3 hi, float &a, float &b) {
+  a = (n.x >= 0.0f ? n.x * lo.x : n.x * hi.x) + (n.y >= 0.0f ? n.y * lo.y : n.y * hi.y) + (n.z >= 0.0f ? n.z * lo.z : n.z * hi.z);
+  b = (n.x >= 0.0f ? n.x * hi.x : n.x * lo.x) + (n.y >= 0.0f ? n.y * hi.y : n.y * lo.y) + (n.z >= 0.0f ? n.z * hi.z : n.z * lo.z);
+}
+__device__ __forceinline__ float absmax(float lo, float hi) { return fmaxf(fabsf(lo), fabsf(hi)); }
+// false: no ray of the bundle can pass always-listed patch k's gate.
+__device__ __forceinline__ bool always_bundle_keep(const float4 *always, uint32_t k, uint32_t n_always, const Bundle &B) {
+  if (k >= n_always) return false;
+  if (!B.finite) return true;
+  constexpr float u = 0x1p-24f;
+  const float4 q0 = always[(size_t)kAlwaysQuads * k], w0 = always[(size_t)kAlwaysQuads * k + 4],
+               w1 = always[(size_t)kAlwaysQuads * k + 5];
+  const f3 n = mk(q0.x, q0.y, q0.z);
+  float csl, csh, nsl, nsh;
+  ivdot(n, B.dlo, B.dhi, csl, csh);
+  ivdot(n, B.slo, B.shi, nsl, nsh);
+  const float mc = 8.0f * u * (fabsf(n.x) * absmax(B.dlo.x, B.dhi.x) + fabsf(n.y) * absmax(B.dlo.y, B.dhi.y) + fabsf(n.z) * absmax(B.dlo.z, B.dhi.z));
+  const float ms = 8.0f * u * (fabsf(n.x) * absmax(B.slo.x, B.shi.x) + fabsf(n.y) * absmax(B.slo.y, B.shi.y) + fabsf(n.z) * absmax(B.slo.z, B.shi.z) + fabsf(q0.w));
+  csl -= mc;
+  csh += mc;
+  const float numl = (q0.w - nsh) - ms, numh = (q0.w - nsl) + ms;
+  if (csl > -0.00001f && csh < 0.00001f) return false;  // |cs| < 1e-5 for every ray
+  if (!(csl > 0.0f || csh < 0.0f)) return true;          // cs of either sign: t unbounded
+  const float r1 = __builtin_amdgcn_rcpf(csl), r2 = __builtin_amdgcn_rcpf(csh);
+  const float a1 = numl * r1, a2 = numl * r2, a3 = numh * r1, a4 = numh * r2;
+  float tlo = fminf(fminf(a1, a2), fminf(a3, a4)), thi = fmaxf(fmaxf(a1, a2), fmaxf(a3, a4));
+  tlo -= 6.0f * u * fabsf(tlo);
+  thi += 6.0f * u * fabsf(thi);
+  if (!(thi <= 1e30f)) return true;  // huge or NaN: no bound
+  if (thi <= 0.0f) return false;     // t > 0 for no ray
+  tlo = fmaxf(tlo, 0.0f);
+  f3 plo, phi;
+  {
+    const float x1 = B.dlo.x * tlo, x2 = B.dlo.x * thi, x3 = B.dhi.x * tlo, x4 = B.dhi.x * thi;
+    plo.x = B.slo.x + fminf(fminf(x1, x2), fminf(x3, x4));
+    phi.x = B.shi.x + fmaxf(fmaxf(x1, x2), fmaxf(x3, x4));
+    const float y1 = B.dlo.y * tlo, y2 = B.dlo.y * thi, y3 = B.dhi.y * tlo, y4 = B.dhi.y * thi;
+    plo.y = B.slo.y + fminf(fminf(y1, y2), fminf(y3, y4));
+    phi.y = B.shi.y + fmaxf(fmaxf(y1, y2), fmaxf(y3, y4));
+    const float z1 = B.dlo.z * tlo, z2 = B.dlo.z * thi, z3 = B.dhi.z * tlo, z4 = B.dhi.z * thi;
+    plo.z = B.slo.z + fminf(fminf(z1, z2), fminf(z3, z4));
+    phi.z = B.shi.z + fmaxf(fmaxf(z1, z2), fmaxf(z3, z4));
+  }
+  const float smax = fmaxf(fmaxf(absmax(B.slo.x, B.shi.x), absmax(B.slo.y, B.shi.y)), absmax(B.slo.z, B.shi.z));
+  const float pm0 = fmaxf(fmaxf(absmax(plo.x, phi.x), absmax(plo.y, phi.y)), absmax(plo.z, phi.z));
+  const float e = 8.0f * u * (smax + pm0);  // the points' own rounding
+  const float pmax = pm0 + e;
+  const f3 w = mk(w0.x, w0.y, w0.z);
+  float wlo, whi;
+  ivdot(w, mk(plo.x - e, plo.y - e, plo.z - e), mk(phi.x + e, phi.y + e, phi.z + e), wlo, whi);
+  const float slack = w1.y * pmax + (w1.z + 64.0f * u) * (smax + pmax);
+  return !(wlo > w1.x + slack) & !(whi < w0.w - slack);
+}
+
 // Candidate search.  `alive` (optional): a ray is traced iff alive[off + i] != BZR_RR_NONE.
 // One wave's 64 rays i (lane l of the wave holds ray i); `stk` is the wave's LDS stack.
 __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__restrict__ rays, uint32_t ld,
@@ -601,14 +694,19 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
     }
   }
   // the always list (patches without a proven gate region, bvh.cpp): gate-tested for every active ray
-  if (__any(active))
-    for (uint32_t k = 0; k < m.n_always; ++k) {
-      uint32_t b;
-      if (always_gate(m.always, k, active, s, d, b)) {
-        if (cnt < kMaxCand) w.cand[(size_t)cnt * n + i] = b;
-        cnt = cnt < kMaxCand ? cnt + 1 : kOverflow;
+  if (m.n_always && __any(active)) {
+    const Bundle bnd = make_bundle(active, s, d);
+    for (uint32_t ab = 0; ab * 64u < m.n_always; ++ab) {
+      unsigned long long am = __ballot(always_bundle_keep(m.always, ab * 64u + (threadIdx.x & 63u), m.n_always, bnd));
+      for (; am; am &= am - 1ull) {
+        uint32_t b;
+        if (always_gate(m.always, ab * 64u + __builtin_ctzll(am), active, s, d, b)) {
+          if (cnt < kMaxCand) w.cand[(size_t)cnt * n + i] = b;
+          cnt = cnt < kMaxCand ? cnt + 1 : kOverflow;
+        }
       }
     }
+  }
   if (count_rays) {  // rays traced (one atomic per wave: on one address, so only with counters on)
     const unsigned long long traced = __ballot(i < n && (alive == nullptr || alive[off + i] != BZR_RR_NONE));
     if ((threadIdx.x & 63u) == 0 && traced) atomicAdd(&w.ctr[2], (uint32_t)__popcll(traced));
@@ -1131,7 +1229,11 @@ __device__ __forceinline__ void trace_segment(const MeshView &m, f3 s, f3 d, boo
   uint32_t scan = kNo;                // next patch of the full scan (kNo: not scanning)
   uint32_t join = kNo, join_src = 0;  // a retry waiting for a later leaf's pass: that leaf, scanned patch
   uint32_t parked_nb = kNo;           // the patch whose cNone result is parked for this lane
-  uint32_t ai = __any(act) ? 0u : m.n_always;  // next always-list record (uniform)
+  // the always list: batches of 64 patches bundle-tested against the wave (uniform state)
+  uint32_t ab = (m.n_always && __any(act)) ? 0u : (m.n_always + 63u) / 64u;  // next batch
+  unsigned long long am = 0ull;  // the current batch's patches left to gate-test
+  Bundle bnd{};
+  if (ab == 0u) bnd = make_bundle(act, s, d);
   for (;;) {
     uint32_t ne = 0;  // collected leaves (uniform)
 #if BZR_TRACE_PRIO
@@ -1179,9 +1281,17 @@ __device__ __forceinline__ void trace_segment(const MeshView &m, f3 s, f3 d, boo
     }
     // tree done: the always list (patches without a proven gate region, bvh.cpp), gate-tested by every
     // wave-segment -- the candidates no box may cull
-    for (; next == kNo && sp == 0 && ai < m.n_always && ne < kEntries; ++ai) {
+    while (next == kNo && sp == 0 && ne < kEntries) {
+      if (am == 0ull) {
+        if (ab * 64u >= m.n_always) break;
+        am = __ballot(always_bundle_keep(m.always, ab * 64u + lane, m.n_always, bnd));
+        ++ab;
+        continue;
+      }
+      const uint32_t k = (ab - 1u) * 64u + __builtin_ctzll(am);
+      am &= am - 1ull;
       uint32_t b;
-      const bool pass = always_gate(m.always, ai, act, s, d, b);
+      const bool pass = always_gate(m.always, k, act, s, d, b);
       if (kCount) {
         ++ctr.leaves;
         ctr.gate_tests += popc64(__ballot(act));

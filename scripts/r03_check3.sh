@@ -4,8 +4,10 @@
 R="$GRAFT_REPO_ROOT"; cd "$R" || exit 2
 OUT="$R/gpurun_out/${TAG:-r03c3}"; mkdir -p "$OUT"
 st() { echo "$1 rc=$2" >> "$OUT/steps.txt"; [ "$2" -ge 124 ] && exit "$2"; return 0; }
-for s in ${STEPS:-pytest smoke bench rehearse sustained configs}; do
+for s in ${STEPS:-ab pytest smoke bench rehearse sustained configs}; do
 case $s in
+ab) for p in staged fused; do timeout -k 10 300 python scripts/ab.py --config cfg5 --pipeline $p --rounds 3 --steps 5 ${AB:-nobundle base} \
+      > "$OUT/ab_cfg5_$p.txt" 2>&1; st "ab $p" $?; done ;;
 pytest) timeout -k 10 900 python -u -m pytest tests -x -v -m gpu -p no:cacheprovider --timeout 120 --timeout-method thread \
           > "$OUT/pytest.log" 2>&1; st pytest $? ;;
 smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1; st smoke $? ;;

@@ -427,3 +427,101 @@ def test_always_wedge_keeps_every_gate_pass(bzr, orc):
             kept, total = int(keep.sum()), keep.size
     assert passes > 100
     assert kept < 0.1 * total  # the config rays: most (ray, always patch) pairs never reach the gate
+
+
+def bundle_keep_f32(patches, wedges, rays):
+    """float32 replica of trace.hip always_bundle_keep: keep[w, k] for waves of 64 consecutive rays
+    (all active) against always-listed patches (records `patches`, wedge words `wedges`)."""
+    f = np.float32
+    u = f(2.0 ** -24)
+    nw = rays.shape[1] // 64
+    r = rays[:, :nw * 64].reshape(6, nw, 64).astype(f)
+    slo, shi = r[:3].min(axis=2).T, r[:3].max(axis=2).T  # [nw, 3]
+    dlo, dhi = r[3:].min(axis=2).T, r[3:].max(axis=2).T
+    fin = np.abs(np.concatenate([slo, shi, dlo, dhi], 1)).max(1) <= f(1e30)
+    S = lambda a: a[:, None, :]  # noqa: E731  [nw, 1, 3]
+    n = patches[None, :, 0:3].astype(f)
+    c = patches[None, :, 3].astype(f)
+
+    def ivdot(v, lo, hi):
+        a = np.where(v >= 0, v * lo, v * hi).astype(f)
+        b = np.where(v >= 0, v * hi, v * lo).astype(f)
+        return (((a[..., 0] + a[..., 1]).astype(f) + a[..., 2]).astype(f),
+                ((b[..., 0] + b[..., 1]).astype(f) + b[..., 2]).astype(f))
+
+    def amax(lo, hi):
+        return np.maximum(np.abs(lo), np.abs(hi))
+
+    with np.errstate(all="ignore"):
+        csl, csh = ivdot(n, S(dlo), S(dhi))
+        nsl, nsh = ivdot(n, S(slo), S(shi))
+        ad, asv = amax(S(dlo), S(dhi)), amax(S(slo), S(shi))
+        mc = (f(8) * u * ((np.abs(n[..., 0]) * ad[..., 0] + np.abs(n[..., 1]) * ad[..., 1]).astype(f) + np.abs(n[..., 2]) * ad[..., 2])).astype(f)
+        ms = (f(8) * u * (((np.abs(n[..., 0]) * asv[..., 0] + np.abs(n[..., 1]) * asv[..., 1]).astype(f) + np.abs(n[..., 2]) * asv[..., 2]).astype(f) + np.abs(c))).astype(f)
+        csl, csh = (csl - mc).astype(f), (csh + mc).astype(f)
+        numl, numh = ((c - nsh) - ms).astype(f), ((c - nsl) + ms).astype(f)
+        tiny = (csl > f(-1e-5)) & (csh < f(1e-5))
+        open_ = ~((csl > 0) | (csh < 0))
+        r1, r2 = (f(1) / csl).astype(f), (f(1) / csh).astype(f)
+        a = np.stack([numl * r1, numl * r2, numh * r1, numh * r2]).astype(f)
+        tlo, thi = np.fmin.reduce(a, 0), np.fmax.reduce(a, 0)
+        tlo = (tlo - f(6) * u * np.abs(tlo)).astype(f)
+        thi = (thi + f(6) * u * np.abs(thi)).astype(f)
+        unb = ~(thi <= f(1e30))
+        neg = thi <= 0
+        tlo = np.maximum(tlo, f(0))
+        plo, phi = [], []
+        for ax in range(3):
+            x = np.stack([S(dlo)[..., ax] * tlo, S(dlo)[..., ax] * thi, S(dhi)[..., ax] * tlo, S(dhi)[..., ax] * thi]).astype(f)
+            plo.append((S(slo)[..., ax] + np.fmin.reduce(x, 0)).astype(f))
+            phi.append((S(shi)[..., ax] + np.fmax.reduce(x, 0)).astype(f))
+        plo, phi = np.stack(plo, -1), np.stack(phi, -1)
+        smax = amax(slo, shi).max(1)[:, None]
+        pm0 = amax(plo, phi).max(-1)
+        e = (f(8) * u * (smax + pm0)).astype(f)
+        pmax = (pm0 + e).astype(f)
+        w = wedges[None, :, 0:3].astype(f)
+        wlo, whi = ivdot(w, plo - e[..., None], phi + e[..., None])
+        slack = (wedges[None, :, 5] * pmax + (wedges[None, :, 6] + f(64) * u) * (smax + pmax)).astype(f)
+        keep = ~(wlo > wedges[None, :, 4] + slack) & ~(whi < wedges[None, :, 3] - slack)
+    keep = np.where(open_ | unb, True, np.where(tiny | neg, False, keep))
+    return np.where(fin[:, None], keep, True)
+
+
+@pytest.mark.slow
+def test_always_bundle_keeps_every_wave_with_a_gate_pass(bzr, orc):
+    """The wave-level bundle test (trace.hip always_bundle_keep) may only drop an always-listed patch for a
+    wave when no ray of that wave passes the patch's gate: cfg5 grid waves (8x8 pixel blocks) and waves of
+    rays aimed at those patches from near the origin (64 rays per target, jittered origins and targets).
+    Most (wave, patch) pairs of the grid are dropped."""
+    cfg = CONFIGS["cfg5"]
+    patches = build_lens(bzr.TriMesh, cfg.lenses[0]).bezier_patches()
+    alw = always_list(bzr, patches, 0)
+    wed = always_wedges(bzr, patches, 0, len(alw))
+    pa = patches[alw]
+    fin = np.isfinite(pa[:, 49:58]).all(axis=1)
+    from bzr_amd.configs import pixel_coords, rays_for
+    rng = np.random.default_rng(31)
+    r, c = pixel_coords(cfg, side=8192, order="tiles")
+    starts = rng.integers(0, len(r) // 64, 600) * 64
+    idx = (starts[:, None] + np.arange(64)[None, :]).reshape(-1)
+    sets = [rays_for(cfg, r[idx], c[idx], side=8192)]
+    for jitter_o, jitter_t in ((0.05, 0.01), (0.5, 0.05)):
+        m = 64 * 400
+        tk = rng.integers(0, fin.sum(), 400).repeat(64)
+        o0 = rng.uniform(-6, 6, (400, 3)).repeat(64, 0)
+        o = o0 + rng.normal(size=(m, 3)) * jitter_o
+        tgt = pa[fin][tk, 19:22] + rng.normal(size=(m, 3)) * jitter_t
+        d = tgt - o
+        d /= np.linalg.norm(d, axis=1, keepdims=True)
+        sets.append(np.concatenate([o.T, d.T]).astype(np.float32))
+    passes = 0
+    for k, rays in enumerate(sets):
+        gate = orc.planar_gate(pa, rays, threads=8).reshape(-1, 64, len(pa)).any(axis=1)
+        keep = bundle_keep_f32(pa, wed, rays)
+        missed = gate & ~keep
+        assert not missed.any(), f"set {k}: {int(missed.sum())} (wave, patch) gate passes dropped"
+        passes += int(gate.sum())
+        if k == 0:
+            assert keep.mean() < 0.15, keep.mean()
+    assert passes > 50
