@@ -38,15 +38,34 @@ import numpy as np
 # depends on the creation / first-use order (torch's pool, the contexts' own streams, RCCL's): with 4, a
 # probe that created its streams in another order saw two slots land on one queue and lose the overlap
 # entirely.  16 queues give every stream here its own.  Set before HIP initialises (torch is imported
-# in main()).  A value the caller already exported is kept (and reported in config.hw_queues).
-_HWQ_SOURCE = "caller" if "GPU_MAX_HW_QUEUES" in os.environ else "bench.py default"
-os.environ.setdefault("GPU_MAX_HW_QUEUES", os.environ.get("BZR_BENCH_HW_QUEUES", "16"))
+# in main()).  set_hw_queues() keeps a caller's value that is large enough (or any value given through
+# BZR_BENCH_HW_QUEUES) and reports the effective one in config.hw_queues.
+HWQ_WANT = 16
+
+
+def set_hw_queues(frames_in_flight: int, world: int) -> str:
+    """GPU_MAX_HW_QUEUES for this run (before HIP initialises): the slots need distinct queues, and HIP's
+    default of 4 (which the GPU pool exports) let two slots share one in a probe.  Returns the source."""
+    explicit = os.environ.get("BZR_BENCH_HW_QUEUES")
+    if explicit:
+        os.environ["GPU_MAX_HW_QUEUES"] = explicit
+        return "BZR_BENCH_HW_QUEUES"
+    have = os.environ.get("GPU_MAX_HW_QUEUES", "")
+    need = max(HWQ_WANT, frames_in_flight + (1 if world > 1 else 0))
+    if have.isdigit() and int(have) >= need:
+        return "caller"
+    os.environ["GPU_MAX_HW_QUEUES"] = str(need)
+    return f"bench.py (raised from {have or 'unset'}: the frame slots need their own queues)"
 
 REPO = Path(__file__).resolve().parent
 sys.path.insert(0, str(REPO / "cuda-bezier-triangle-raytracer_amd"))
 sys.path.insert(0, str(REPO))
 
 VALU_PEAK_TFLOPS = 157.3      # MI355X FP32 vector peak (MI355X_MICROARCH.md, chip parameters)
+PEAK_CLOCK_GHZ = 2.4          # the clock the peaks above are quoted at
+SIMDS, CUS = 1024, 256        # 256 CUs x 4 SIMDs
+VALU_ISSUE_PEAK = SIMDS * PEAK_CLOCK_GHZ / 2.0  # G wave64 VALU instructions/s (one per 2 cycles per SIMD)
+SALU_ISSUE_PEAK = CUS * PEAK_CLOCK_GHZ          # G scalar instructions/s (one scalar unit per CU)
 HBM_PEAK_GBS = 8000.0         # MI355X HBM3E peak (spec)
 FLOPS_PLANAR = 33.0           # algorithmic flops per (segment, patch) planar gate (SURVEY.md 8d)
 FLOPS_NEWTON = 1750.0         # algorithmic flops per Newton run: bracket + 4 iterations + tail (SURVEY.md 8a a6)
@@ -157,6 +176,19 @@ def cpu_baseline(cfg, side, patches, ris, stride, runs):
     return line, cnt
 
 
+def pmc_issue(kernel, workload):
+    """Issue counts per launch of `kernel` (SQ_INSTS_VALU / _SALU / _SMEM, SQ_WAVES) from the committed PMC
+    profile of this workload (profiles/pmc_traffic.json), or None."""
+    path = REPO / "profiles" / "pmc_traffic.json"
+    if not path.exists():
+        return None
+    d = json.loads(path.read_text()).get("workloads", {}).get(workload)
+    k = d and d["kernels"].get(kernel)
+    if not k or "valu_insts" not in k:
+        return None
+    return dict(k, source=d["source"])
+
+
 def pmc_traffic(kernel, workload):
     """HBM bytes per launch of `kernel` from the committed PMC profile of this workload
     (profiles/pmc_traffic.json, written by scripts/prof_summary.py from rocprofv3 FETCH_SIZE (x2, gfx950
@@ -176,6 +208,9 @@ def pmc_traffic(kernel, workload):
 
 def main():
     a = parse()
+    if a.inflight <= 0:  # the staged pipeline's small kernels contend beyond two frames (DESIGN.md (a))
+        a.inflight = 3 if (a.accel == "bvh" and a.pipeline == "fused") else 2
+    hwq_source = set_hw_queues(a.inflight, int(os.environ.get("WORLD_SIZE", "1")))
     import torch
     import torch.distributed as dist
 
@@ -210,8 +245,6 @@ def main():
     upload_s = time.perf_counter() - t0
     # one stream per frame slot (--inflight); GPU_MAX_HW_QUEUES (top of this file) gives each its own
     # hardware queue, so the slots' frames overlap
-    if a.inflight <= 0:  # the staged pipeline's small kernels contend beyond two frames (DESIGN.md (a))
-        a.inflight = 3 if (a.accel == "bvh" and a.pipeline == "fused") else 2
     streams = [torch.cuda.Stream(dev) for _ in range(max(1, a.inflight))]
     hwq = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
     if hwq < len(streams) + (1 if world > 1 else 0) and rank == 0:
@@ -377,6 +410,27 @@ def main():
         workload_key = f"{cfg.name}/{a.pipeline}/{a.mode}/{side}"
         traffic, traffic_src = pmc_traffic(dom, workload_key) if world == 1 else (None, None)
         launches = d["launches_per_step"]
+        roof = {"bound": "valu", "kernel": dom, "achieved": achieved, "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": None if achieved is None else round(achieved / VALU_PEAK_TFLOPS, 4)}
+        iss = pmc_issue(dom, workload_key) if (achieved is None and world == 1) else None
+        if iss is not None:
+            # no flop model (the BVH walk: bookkeeping, slab tests, scalar loads): an issue roof instead --
+            # the kernel's VALU and SALU instructions per launch (committed PMC) over its HIP-event launch
+            # time, against one wave64 VALU instruction per 2 cycles per SIMD and one SALU instruction per
+            # cycle per CU at the 2.4 GHz peak clock; the busier unit is the bound
+            sec = d["avg_launch_ms"] * 1e-3
+            v_rate, s_rate = iss["valu_insts"] / sec / 1e9, iss["salu_insts"] / sec / 1e9
+            vf, sf = v_rate / VALU_ISSUE_PEAK, s_rate / SALU_ISSUE_PEAK
+            roof = {"bound": "valu-issue" if vf >= sf else "salu-issue", "kernel": dom,
+                    "achieved": round(v_rate if vf >= sf else s_rate, 3),
+                    "peak": VALU_ISSUE_PEAK if vf >= sf else SALU_ISSUE_PEAK, "unit": "G instructions/s",
+                    "frac": round(max(vf, sf), 4),
+                    "issue": {"valu_frac": round(vf, 4), "salu_frac": round(sf, 4),
+                              "valu_insts_per_launch": iss["valu_insts"], "salu_insts_per_launch": iss["salu_insts"],
+                              "smem_insts_per_launch": iss.get("smem_insts"), "waves_per_launch": iss.get("waves"),
+                              "source": iss["source"],
+                              "node_visits_per_wave_segment": round(work_cnt["node_visits"] * 64 / segs, 3),
+                              "leaf_fetches_per_wave_segment": round(work_cnt["leaf_fetches"] * 64 / segs, 3)}}
         line = {
             "metric": "Mrays/sec (primary+refracted) at 1/2/4/8 MI355X; % of HBM-read roofline",
             "value": round(value, 3),
@@ -404,7 +458,7 @@ def main():
                            if gather else None),
                 "pipeline": a.pipeline,
                 "frames_in_flight": F,
-                "hw_queues": {"GPU_MAX_HW_QUEUES": hwq, "source": _HWQ_SOURCE,
+                "hw_queues": {"GPU_MAX_HW_QUEUES": hwq, "source": hwq_source,
                               "streams": len(streams) + (1 if gather else 0),
                               "ok": hwq >= len(streams) + (1 if gather else 0)},
                 "scan": "BVH-culled (bit-identical to brute force)" if a.accel == "bvh" else "brute force",
@@ -414,12 +468,7 @@ def main():
                 "upload_and_bvh_s": round(upload_s, 3),
             },
             "roofline": {
-                "bound": "valu",
-                "kernel": dom,
-                "achieved": achieved,
-                "peak": VALU_PEAK_TFLOPS,
-                "unit": "TFLOP/s",
-                "frac": None if achieved is None else round(achieved / VALU_PEAK_TFLOPS, 4),
+                **roof,
                 "traffic": traffic,
                 "traffic_unit": "HBM bytes per launch (PMC)",
                 "traffic_source": traffic_src,

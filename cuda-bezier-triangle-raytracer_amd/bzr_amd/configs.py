@@ -116,12 +116,13 @@ def grid_rays(cfg: Config, side: int | None = None, order: str = "tiles") -> np.
 
 
 def shard_pixels(cfg: Config, rank: int, world: int, side: int | None = None, height: int | None = None,
-                 block: int = 64):
+                 block: int = 64, order: str = "centre"):
     """Image-plane sharding for multi-GPU runs over a side-wide, height-tall image: block x block pixel
     tiles dealt round-robin (tile k -> rank k % world), each tile walked in 8x8 sub-tiles (one 64-ray
     wavefront each).  A rank's tiles are listed nearest the image centre first: the lens-hitting tiles,
     whose waves run longest, are dispatched first and the frame ends on short missing waves (cfg4, one
-    frame in flight: 5.00 -> 4.76 ms).  Returns (rows, cols) of this rank's pixels."""
+    frame in flight, scripts/tile_order_probe.py).  order="dealt" keeps the plain dealing order (the probe's
+    baseline).  Returns (rows, cols) of this rank's pixels."""
     s = cfg.side if side is None else side
     h = s if height is None else height
     if s % block or h % block:
@@ -130,7 +131,10 @@ def shard_pixels(cfg: Config, rank: int, world: int, side: int | None = None, he
     tiles = np.arange(nbx * nby)[rank::world]
     dy = (tiles // nbx + 0.5) * block - h / 2
     dx = (tiles % nbx + 0.5) * block - s / 2
-    tiles = tiles[np.argsort(dy * dy + dx * dx, kind="stable")]
+    if order == "centre":
+        tiles = tiles[np.argsort(dy * dy + dx * dx, kind="stable")]
+    elif order != "dealt":
+        raise ValueError(f"order {order!r}")
     sub_r, sub_c = pixel_coords(cfg, block, "tiles")
     rows = ((tiles // nbx)[:, None] * block + sub_r[None, :]).reshape(-1)
     cols = ((tiles % nbx)[:, None] * block + sub_c[None, :]).reshape(-1)

@@ -124,6 +124,9 @@ constexpr uint32_t kOverflow = 0xFFFFu;  // count value: resolve with the full s
 #define BZR_STACK 64
 #endif
 constexpr int kStack = BZR_STACK;
+// Device work counters (bzr_ctx_counters) are kept in this many copies, summed by the report: a wave adds
+// to copy (wave index mod kCounterReplicas), so a frame's ~10^5 waves do not queue on a few addresses.
+constexpr uint32_t kCounterReplicas = 64;
 
 // 64-byte wave-uniform records read through the constant address space: one s_load_dwordx16 each
 typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
@@ -555,33 +558,56 @@ __device__ __forceinline__ bool always_gate(const float4 *always, uint32_t k, bo
 // patches per VALU instruction instead of one.  Every margin rounds outward (u = 2^-24): the lanes' dot
 // products 8u, the corner quotients 6u, the points 8u, the wedge product and the bound 64u of (|S| + |P|).
 // Non-finite bundles (or t ranges beyond 1e30) keep everything.
-struct Bundle {
-  f3 slo, shi, dlo, dhi;
-  bool finite;
-};
+// The bundle lives in LDS (13 words per wave: slo, shi, dlo, dhi, finite flag) and is read at its points of
+// use (volatile: not hoisted): in registers it stayed live across the fused kernel's walk and cost two
+// waves per SIMD of occupancy (69 -> 98 VGPRs).
+// Wave min / max by ds_swizzle (xor within 32 lanes; the pattern is an immediate, so no lane-index
+// registers -- __shfl_xor's bpermute addresses were hoisted and kept 5 VGPRs live across the whole kernel)
+// and the two halves combined through readlane: the result is uniform.
+template <int kXor>
+__device__ __forceinline__ float swz(float v) {
+  return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 0x1F | (kXor << 10)));
+}
+__device__ __forceinline__ float halves(float v, bool mx) {
+  const float a = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+  const float b = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+  return mx ? fmaxf(a, b) : fminf(a, b);
+}
 __device__ __forceinline__ float wave_minf(float v) {
-#pragma unroll
-  for (int k = 32; k >= 1; k >>= 1) v = fminf(v, __shfl_xor(v, k, 64));
-  return v;
+  v = fminf(v, swz<1>(v));
+  v = fminf(v, swz<2>(v));
+  v = fminf(v, swz<4>(v));
+  v = fminf(v, swz<8>(v));
+  v = fminf(v, swz<16>(v));
+  return halves(v, false);
 }
 __device__ __forceinline__ float wave_maxf(float v) {
-#pragma unroll
-  for (int k = 32; k >= 1; k >>= 1) v = fmaxf(v, __shfl_xor(v, k, 64));
-  return v;
+  v = fmaxf(v, swz<1>(v));
+  v = fmaxf(v, swz<2>(v));
+  v = fmaxf(v, swz<4>(v));
+  v = fmaxf(v, swz<8>(v));
+  v = fmaxf(v, swz<16>(v));
+  return halves(v, true);
 }
-__device__ __forceinline__ Bundle make_bundle(bool act, f3 s, f3 d) {
+// The 12 reductions one after another (a loop that is not unrolled), each stored to the wave's LDS words as
+// soon as it is done, so only one is in registers at a time; word 12 = 1 when every box bound is finite
+// (false also for an empty bundle, whose boxes are +-inf).
+constexpr uint32_t kBundleWords = 13;
+__device__ __forceinline__ void bundle_to_lds(bool act, f3 s, f3 d, float *out, uint32_t lane) {
   const float inf = __builtin_inff();
-  Bundle b;
-  b.slo = mk(wave_minf(act ? s.x : inf), wave_minf(act ? s.y : inf), wave_minf(act ? s.z : inf));
-  b.shi = mk(wave_maxf(act ? s.x : -inf), wave_maxf(act ? s.y : -inf), wave_maxf(act ? s.z : -inf));
-  b.dlo = mk(wave_minf(act ? d.x : inf), wave_minf(act ? d.y : inf), wave_minf(act ? d.z : inf));
-  b.dhi = mk(wave_maxf(act ? d.x : -inf), wave_maxf(act ? d.y : -inf), wave_maxf(act ? d.z : -inf));
-  const float m = fmaxf(fmaxf(fmaxf(fabsf(b.slo.x), fabsf(b.slo.y)), fmaxf(fabsf(b.slo.z), fabsf(b.shi.x))),
-                        fmaxf(fmaxf(fabsf(b.shi.y), fabsf(b.shi.z)),
-                              fmaxf(fmaxf(fabsf(b.dlo.x), fabsf(b.dlo.y)), fmaxf(fmaxf(fabsf(b.dlo.z), fabsf(b.dhi.x)),
-                                                                               fmaxf(fabsf(b.dhi.y), fabsf(b.dhi.z))))));
-  b.finite = m <= 1e30f;  // also false for an empty bundle (every box +-inf)
-  return b;
+  float m = 0.0f;
+#pragma unroll 1
+  for (uint32_t k = 0; k < 12u; ++k) {
+    const uint32_t a = k % 3u;
+    const f3 v = k < 6u ? s : d;
+    const float x = a == 0u ? v.x : (a == 1u ? v.y : v.z);
+    const bool lo = (k / 3u) % 2u == 0u;
+    const float r = lo ? wave_minf(act ? x : inf) : wave_maxf(act ? x : -inf);
+    m = fmaxf(m, fabsf(r));
+    if (lane == 0u) out[k] = r;
+  }
+  if (lane == 0u) out[12] = m <= 1e30f ? 1.0f : 0.0f;
+  __builtin_amdgcn_wave_barrier();  // the words are read back by every lane of this wave
 }
 // Interval of n.x over x in [lo, hi] (n fixed).
 __device__ __forceinline__ void ivdot(f3 n, f3 lo, f3 hi, float &a, float &b) {
@@ -589,19 +615,19 @@ __device__ __forceinline__ void ivdot(f3 n, f3 lo, f3 hi, float &a, float &b) {
   b = (n.x >= 0.0f ? n.x * hi.x : n.x * lo.x) + (n.y >= 0.0f ? n.y * hi.y : n.y * lo.y) + (n.z >= 0.0f ? n.z * hi.z : n.z * lo.z);
 }
 __device__ __forceinline__ float absmax(float lo, float hi) { return fmaxf(fabsf(lo), fabsf(hi)); }
-// false: no ray of the bundle can pass always-listed patch k's gate.
-__device__ __forceinline__ bool always_bundle_keep(const float4 *always, uint32_t k, uint32_t n_always, const Bundle &B) {
+// false: no ray of the bundle (LDS words bl) can pass always-listed patch k's gate.
+__device__ __forceinline__ bool always_bundle_keep(const float4 *always, uint32_t k, uint32_t n_always, const float *bl) {
   if (k >= n_always) return false;
-  if (!B.finite) return true;
+  const float *B = bl;
+  if (!(B[12] > 0.0f)) return true;
   constexpr float u = 0x1p-24f;
-  const float4 q0 = always[(size_t)kAlwaysQuads * k], w0 = always[(size_t)kAlwaysQuads * k + 4],
-               w1 = always[(size_t)kAlwaysQuads * k + 5];
+  const float4 q0 = always[(size_t)kAlwaysQuads * k];
   const f3 n = mk(q0.x, q0.y, q0.z);
   float csl, csh, nsl, nsh;
-  ivdot(n, B.dlo, B.dhi, csl, csh);
-  ivdot(n, B.slo, B.shi, nsl, nsh);
-  const float mc = 8.0f * u * (fabsf(n.x) * absmax(B.dlo.x, B.dhi.x) + fabsf(n.y) * absmax(B.dlo.y, B.dhi.y) + fabsf(n.z) * absmax(B.dlo.z, B.dhi.z));
-  const float ms = 8.0f * u * (fabsf(n.x) * absmax(B.slo.x, B.shi.x) + fabsf(n.y) * absmax(B.slo.y, B.shi.y) + fabsf(n.z) * absmax(B.slo.z, B.shi.z) + fabsf(q0.w));
+  ivdot(n, mk(B[6], B[7], B[8]), mk(B[9], B[10], B[11]), csl, csh);
+  ivdot(n, mk(B[0], B[1], B[2]), mk(B[3], B[4], B[5]), nsl, nsh);
+  const float mc = 8.0f * u * (fabsf(n.x) * absmax(B[6], B[9]) + fabsf(n.y) * absmax(B[7], B[10]) + fabsf(n.z) * absmax(B[8], B[11]));
+  const float ms = 8.0f * u * (fabsf(n.x) * absmax(B[0], B[3]) + fabsf(n.y) * absmax(B[1], B[4]) + fabsf(n.z) * absmax(B[2], B[5]) + fabsf(q0.w));
   csl -= mc;
   csh += mc;
   const float numl = (q0.w - nsh) - ms, numh = (q0.w - nsl) + ms;
@@ -615,25 +641,28 @@ __device__ __forceinline__ bool always_bundle_keep(const float4 *always, uint32_
   if (!(thi <= 1e30f)) return true;  // huge or NaN: no bound
   if (thi <= 0.0f) return false;     // t > 0 for no ray
   tlo = fmaxf(tlo, 0.0f);
-  f3 plo, phi;
-  {
-    const float x1 = B.dlo.x * tlo, x2 = B.dlo.x * thi, x3 = B.dhi.x * tlo, x4 = B.dhi.x * thi;
-    plo.x = B.slo.x + fminf(fminf(x1, x2), fminf(x3, x4));
-    phi.x = B.shi.x + fmaxf(fmaxf(x1, x2), fmaxf(x3, x4));
-    const float y1 = B.dlo.y * tlo, y2 = B.dlo.y * thi, y3 = B.dhi.y * tlo, y4 = B.dhi.y * thi;
-    plo.y = B.slo.y + fminf(fminf(y1, y2), fminf(y3, y4));
-    phi.y = B.shi.y + fmaxf(fmaxf(y1, y2), fmaxf(y3, y4));
-    const float z1 = B.dlo.z * tlo, z2 = B.dlo.z * thi, z3 = B.dhi.z * tlo, z4 = B.dhi.z * thi;
-    plo.z = B.slo.z + fminf(fminf(z1, z2), fminf(z3, z4));
-    phi.z = B.shi.z + fmaxf(fmaxf(z1, z2), fmaxf(z3, z4));
+  // plane points P = S + D T and the wedge w.P, one axis at a time
+  const float4 w0 = always[(size_t)kAlwaysQuads * k + 4];
+  float wlo = 0.0f, whi = 0.0f, pm0 = 0.0f, smax = 0.0f, wabs = 0.0f;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    const float dl = B[6 + a], dh = B[9 + a], sl = B[a], sh = B[3 + a];
+    const float x1 = dl * tlo, x2 = dl * thi, x3 = dh * tlo, x4 = dh * thi;
+    const float pl = sl + fminf(fminf(x1, x2), fminf(x3, x4)), ph = sh + fmaxf(fmaxf(x1, x2), fmaxf(x3, x4));
+    const float wa = a == 0 ? w0.x : (a == 1 ? w0.y : w0.z);
+    wlo += wa >= 0.0f ? wa * pl : wa * ph;
+    whi += wa >= 0.0f ? wa * ph : wa * pl;
+    wabs += fabsf(wa);
+    pm0 = fmaxf(pm0, absmax(pl, ph));
+    smax = fmaxf(smax, absmax(sl, sh));
   }
-  const float smax = fmaxf(fmaxf(absmax(B.slo.x, B.shi.x), absmax(B.slo.y, B.shi.y)), absmax(B.slo.z, B.shi.z));
-  const float pm0 = fmaxf(fmaxf(absmax(plo.x, phi.x), absmax(plo.y, phi.y)), absmax(plo.z, phi.z));
-  const float e = 8.0f * u * (smax + pm0);  // the points' own rounding
+  // the points' own rounding e on every axis moves w.P by at most |w|_1 e; the wedge product's and the
+  // bound's rounding are inside 64 u (|S| + |P|)
+  const float e = 8.0f * u * (smax + pm0);
   const float pmax = pm0 + e;
-  const f3 w = mk(w0.x, w0.y, w0.z);
-  float wlo, whi;
-  ivdot(w, mk(plo.x - e, plo.y - e, plo.z - e), mk(phi.x + e, phi.y + e, phi.z + e), wlo, whi);
+  wlo -= wabs * e;
+  whi += wabs * e;
+  const float4 w1 = always[(size_t)kAlwaysQuads * k + 5];
   const float slack = w1.y * pmax + (w1.z + 64.0f * u) * (smax + pmax);
   return !(wlo > w1.x + slack) & !(whi < w0.w - slack);
 }
@@ -642,7 +671,9 @@ __device__ __forceinline__ bool always_bundle_keep(const float4 *always, uint32_
 // One wave's 64 rays i (lane l of the wave holds ray i); `stk` is the wave's LDS stack.
 __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__restrict__ rays, uint32_t ld,
                                               uint32_t off, const uint32_t *__restrict__ alive, uint32_t n,
-                                              const Work &w, uint32_t count_rays, uint32_t i, uint32_t *stk) {
+                                              const Work &w, unsigned long long *counters, uint32_t i, uint32_t *stk,
+                                              float *bl) {
+  uint32_t c_nodes = 0, c_leaves = 0, c_gates = 0;  // work counters (with counters on; wave-uniform)
   bool active = i < n && (alive == nullptr || alive[off + i] != BZR_RR_NONE);
   f3 s = mk(0.0f, 0.0f, 0.0f), d = s;
   if (i < n) load_ray(rays, ld, off + i, s, d);
@@ -666,6 +697,7 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
   while (next != 0xFFFFFFFFu || sp > 0) {
     const uint32_t node = next != 0xFFFFFFFFu ? next : __builtin_amdgcn_readfirstlane(stk[--sp]);
     next = 0xFFFFFFFFu;
+    if (counters) ++c_nodes;
     bool hit[4];
     uint32_t ch[4];
     node_children(nodes, obb, node, active, s, d, sinv, inv, hit, ch);
@@ -679,6 +711,10 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
         const float4 q1 = make_float4(__uint_as_float(r[4]), __uint_as_float(r[5]), __uint_as_float(r[6]), __uint_as_float(r[7]));
         const float4 q2 = make_float4(__uint_as_float(r[8]), __uint_as_float(r[9]), __uint_as_float(r[10]), __uint_as_float(r[11]));
         const float4 q3 = make_float4(__uint_as_float(r[12]), __uint_as_float(r[13]), __uint_as_float(r[14]), 0.0f);
+        if (counters) {
+          ++c_leaves;
+          c_gates += (uint32_t)__popcll(hm);
+        }
         if (hit[c] & planar_gate(q0, q1, q2, q3, s, d)) {
           if (cnt < kMaxCand) w.cand[(size_t)cnt * n + i] = r[15];
           cnt = cnt < kMaxCand ? cnt + 1 : kOverflow;
@@ -695,11 +731,15 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
   }
   // the always list (patches without a proven gate region, bvh.cpp): gate-tested for every active ray
   if (m.n_always && __any(active)) {
-    const Bundle bnd = make_bundle(active, s, d);
+    bundle_to_lds(active, s, d, bl, threadIdx.x & 63u);
     for (uint32_t ab = 0; ab * 64u < m.n_always; ++ab) {
-      unsigned long long am = __ballot(always_bundle_keep(m.always, ab * 64u + (threadIdx.x & 63u), m.n_always, bnd));
+      unsigned long long am = __ballot(always_bundle_keep(m.always, ab * 64u + (threadIdx.x & 63u), m.n_always, bl));
       for (; am; am &= am - 1ull) {
         uint32_t b;
+        if (counters) {
+          ++c_leaves;
+          c_gates += (uint32_t)__popcll(__ballot(active));
+        }
         if (always_gate(m.always, ab * 64u + __builtin_ctzll(am), active, s, d, b)) {
           if (cnt < kMaxCand) w.cand[(size_t)cnt * n + i] = b;
           cnt = cnt < kMaxCand ? cnt + 1 : kOverflow;
@@ -707,9 +747,14 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
       }
     }
   }
-  if (count_rays) {  // rays traced (one atomic per wave: on one address, so only with counters on)
+  if (counters) {  // rays traced (one atomic per wave: on one address, so only with counters on)
     const unsigned long long traced = __ballot(i < n && (alive == nullptr || alive[off + i] != BZR_RR_NONE));
     if ((threadIdx.x & 63u) == 0 && traced) atomicAdd(&w.ctr[2], (uint32_t)__popcll(traced));
+    // walk work (bzr_ctx_counters node_visits / leaf_fetches / gate_tests), spread over the replicas
+    const uint32_t lane = threadIdx.x & 63u, rep = (i >> 6) % kCounterReplicas;
+    const uint32_t v = lane == 0u ? c_nodes : (lane == 1u ? c_leaves : c_gates);
+    const uint32_t which = lane == 0u ? BZR_COUNTER_NODE_VISITS : (lane == 1u ? BZR_COUNTER_LEAF_FETCHES : BZR_COUNTER_GATE_TESTS);
+    if (lane < 3u && v) atomicAdd(&counters[(size_t)rep * BZR_COUNTER_COUNT + which], (unsigned long long)v);
   }
   if (i >= n) return;
   w.count[i] = cnt;
@@ -768,10 +813,12 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
 #endif
 __global__ __launch_bounds__(kTravBlock) void k_traverse(MeshView m, const float *__restrict__ rays, uint32_t ld,
                                                          uint32_t off, const uint32_t *__restrict__ alive, uint32_t n,
-                                                         Work w, uint32_t count_rays) {
+                                                         Work w, unsigned long long *counters) {
   __shared__ uint32_t stack[kTravBlock / 64][kStack];
+  __shared__ float bundle[kTravBlock / 64][kBundleWords];  // the wave's always-list bundle (always_bundle_keep)
   const uint32_t b = deal_blocks<BZR_TRAV_XCD>(blockIdx.x, gridDim.x);
-  traverse_rays(m, rays, ld, off, alive, n, w, count_rays, b * kTravBlock + threadIdx.x, stack[threadIdx.x >> 6]);
+  traverse_rays(m, rays, ld, off, alive, n, w, counters, b * kTravBlock + threadIdx.x, stack[threadIdx.x >> 6],
+                bundle[threadIdx.x >> 6]);
 }
 
 
@@ -1076,9 +1123,6 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_small(uint32_t *__restric
 // that need neither idle through it (lane utilisation).  Rays whose origin lies beyond the
 // tree's validity radius, or whose stack overflows, take the reference's in-order scan in the same wave
 // (same Newton site, patches in index order).
-// Device work counters (bzr_ctx_counters) are kept in this many copies, summed by the report: a wave adds
-// to copy (wave index mod kCounterReplicas), so a frame's ~10^5 waves do not queue on 8 addresses.
-constexpr uint32_t kCounterReplicas = 64;
 struct TraceCtr {  // wave-uniform work counters (kCount)
   uint32_t nodes = 0, leaves = 0, gate_tests = 0, rounds = 0, pairs = 0, follows = 0, segments = 0, ovf = 0;
 };
@@ -1108,6 +1152,7 @@ struct TraceLds {  // per wave
   uint32_t stack[kStack];
   float hit[TraceWords<kMode>::kHit][64];    // the lane's current winner (written only when it improves)
   unsigned long long emask[kEntries];        // collected leaves: gate ballot
+  float bundle[kBundleWords];                // the always list's ray bundle (always_bundle_keep)
   uint32_t eid[kEntries];                    // and patch index
   float park[TraceWords<kMode>::kPark ? TraceWords<kMode>::kPark : 1][64];
 };
@@ -1229,11 +1274,10 @@ __device__ __forceinline__ void trace_segment(const MeshView &m, f3 s, f3 d, boo
   uint32_t scan = kNo;                // next patch of the full scan (kNo: not scanning)
   uint32_t join = kNo, join_src = 0;  // a retry waiting for a later leaf's pass: that leaf, scanned patch
   uint32_t parked_nb = kNo;           // the patch whose cNone result is parked for this lane
-  // the always list: batches of 64 patches bundle-tested against the wave (uniform state)
+  // the always list: batches of 64 patches bundle-tested against the wave (uniform state; the bundle is
+  // built once per segment into LDS, so no register holds it across the walk and the Newton passes)
   uint32_t ab = (m.n_always && __any(act)) ? 0u : (m.n_always + 63u) / 64u;  // next batch
   unsigned long long am = 0ull;  // the current batch's patches left to gate-test
-  Bundle bnd{};
-  if (ab == 0u) bnd = make_bundle(act, s, d);
   for (;;) {
     uint32_t ne = 0;  // collected leaves (uniform)
 #if BZR_TRACE_PRIO
@@ -1284,7 +1328,8 @@ __device__ __forceinline__ void trace_segment(const MeshView &m, f3 s, f3 d, boo
     while (next == kNo && sp == 0 && ne < kEntries) {
       if (am == 0ull) {
         if (ab * 64u >= m.n_always) break;
-        am = __ballot(always_bundle_keep(m.always, ab * 64u + lane, m.n_always, bnd));
+        if (ab == 0u) bundle_to_lds(act, s, d, L.bundle, lane);
+        am = __ballot(always_bundle_keep(m.always, ab * 64u + lane, m.n_always, L.bundle));
         ++ab;
         continue;
       }
@@ -1420,9 +1465,11 @@ struct TraceJob {
   uint32_t wave_real;              // wave_clock holds [4 * waves]: + s_memrealtime start, duration (100 MHz)
 };
 
-// BZR_TRACE_WPE (A/B knob, default 0 = the compiler's choice): amdgpu_waves_per_eu lower bound for k_trace.
+// BZR_TRACE_WPE (default 6): amdgpu_waves_per_eu lower bound for k_trace.  The chain kernel needs 72 VGPRs
+// (7 waves per SIMD) by itself; the intersect kernel (kModeHits: a 12-word winner) would take 82 (5 waves)
+// since the always list's bundle code, and the bound holds it at 80 (6 waves, as before) without scratch.
 #ifndef BZR_TRACE_WPE
-#define BZR_TRACE_WPE 0
+#define BZR_TRACE_WPE 6
 #endif
 #if BZR_TRACE_WPE
 #define BZR_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(BZR_TRACE_WPE)))
@@ -1815,7 +1862,7 @@ bzr_status run_culled(bzr_ctx *ctx, const MeshView &mv, const float *rays, uint3
                            ctx->stream));
   ctx->zero_ctr = nullptr;  // valid again only once this segment is fully enqueued
   launch_on(ctx, ctx->stream, dim3(kTravBlock), BZR_KERNEL_TRAVERSE, k_traverse, dim3((n + kTravBlock - 1) / kTravBlock),
-            mv, rays, ld, off, alive, n, w, uint32_t(ctx->counting ? 1u : 0u));
+            mv, rays, ld, off, alive, n, w, (ctx->counting && ctx->counters) ? ctx->counters : nullptr);
   {
     Span sp(ctx, BZR_KERNEL_BUCKET);
     if (small_scan)

@@ -110,6 +110,11 @@ def write_traffic(p, source, out, workload):
             e["read"] = 2 * c["FETCH_SIZE"] * 1024
         if "WRITE_SIZE" in c:
             e["write"] = c["WRITE_SIZE"] * 1024
+        # issue counts per launch (bench.py's issue roof for kernels without a flop model, e.g. k_traverse)
+        for cn, key in (("SQ_INSTS_VALU", "valu_insts"), ("SQ_INSTS_SALU", "salu_insts"), ("SQ_INSTS_SMEM", "smem_insts"),
+                        ("SQ_WAVES", "waves")):
+            if cn in c:
+                e[key] = c[cn]
         if e:
             kern[k] = e
     path = Path(out)
@@ -117,7 +122,8 @@ def write_traffic(p, source, out, workload):
     d.setdefault("workloads", {})
     d["unit"] = "HBM bytes per launch"
     d["workloads"][workload] = {"source": source, "kernels": kern,
-                                "method": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950 correction) and WRITE_SIZE, separate passes"}
+                                "method": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950 correction) and WRITE_SIZE, separate passes; "
+                                          "SQ_INSTS_VALU / SQ_INSTS_SALU / SQ_INSTS_SMEM / SQ_WAVES per launch from the SQ passes"}
     path.write_text(json.dumps(d, indent=1) + "\n")
     print(f"wrote {out}: {workload}: {len(kern)} kernels")
 

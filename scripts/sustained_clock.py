@@ -20,7 +20,8 @@ import sys
 import time
 from pathlib import Path
 
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+if not os.environ.get("GPU_MAX_HW_QUEUES", "").isdigit() or int(os.environ["GPU_MAX_HW_QUEUES"]) < 16:
+    os.environ["GPU_MAX_HW_QUEUES"] = "16"  # the frame slots need their own hardware queues (bench.py)
 REPO = Path(__file__).resolve().parents[1]
 sys.path[:0] = [str(REPO / "cuda-bezier-triangle-raytracer_amd"), str(REPO)]
 
@@ -91,6 +92,7 @@ def main():
     line = {
         "workload": "cfg4 4096^2 two-lens chain, fused, parity",
         "frames_in_flight": F,
+        "GPU_MAX_HW_QUEUES": os.environ.get("GPU_MAX_HW_QUEUES"),
         "segments_per_frame": segs,
         "sustained_s": round(total_s, 3),
         "frames": a.window * len(windows),

@@ -69,7 +69,7 @@ def wave_cost(rows, cols):
 
 
 for world in (1, 2, 4, 8):
-    rows, cols = shard_pixels(cfg, 0, world, side=side)
+    rows, cols = shard_pixels(cfg, 0, world, side=side, order="dealt")  # tiles k = rank, rank + world, ...
     res = {}
     seg = tile_segments(rows, cols)
     cy = rows.reshape(-1, 4096).mean(axis=1) - side / 2
