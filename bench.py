@@ -431,6 +431,16 @@ def main():
                               "source": iss["source"],
                               "node_visits_per_wave_segment": round(work_cnt["node_visits"] * 64 / segs, 3),
                               "leaf_fetches_per_wave_segment": round(work_cnt["leaf_fetches"] * 64 / segs, 3)}}
+        # VALU issue over the frame interval with frames in flight: the committed PMC instruction count of
+        # the dominant kernel per launch x launches per step, one wave64 VALU instruction per 2 cycles per
+        # SIMD at the 2.4 GHz peak clock, over ms_per_step (the serialized per-launch view above idles
+        # through each frame's tail; this is what the overlapped frames keep the SIMDs busy with)
+        iss_all = pmc_issue(dom, workload_key) if world == 1 else None
+        if iss_all is not None:
+            roof["valu_issue_in_flight"] = {
+                "frac": round(iss_all["valu_insts"] * launches * 2.0 / (SIMDS * PEAK_CLOCK_GHZ * 1e9 * ms_per_step * 1e-3), 4),
+                "valu_insts_per_step": round(iss_all["valu_insts"] * launches), "source": iss_all["source"],
+                "note": "VALU instructions per step (PMC) x 2 cycles / (1024 SIMDs x 2.4 GHz x ms_per_step)"}
         line = {
             "metric": "Mrays/sec (primary+refracted) at 1/2/4/8 MI355X; % of HBM-read roofline",
             "value": round(value, 3),

@@ -423,7 +423,9 @@ __device__ __forceinline__ void node_children(const bzr_host::Bvh4Node *nodes, c
 //               histogram (rank of each (ray, patch) pair within its patch bucket) and the list
 //               of rays that need the full scan (list/stack overflow, origin beyond s_max)
 //   scan        exclusive sum of the histogram (hipCUB) -> bucket offsets, total pair count
-//   k_scatter   (ray, patch) pairs into patch-major order
+//   k_scatter   (ray, patch) pairs into patch-major order (8-byte records: the Newton stage reads the
+//               ray itself from the ray array -- neighbouring rays, mostly cached -- instead of a 32-byte
+//               copy travelling with the pair)
 //   k_newton    the Newton stage per pair; a wave holds <= a few distinct patches, processed one at a
 //               time with the patch record in scalar registers (uniform loads); hits go to a per-pair
 //               slot and a per-ray 64-bit atomicMin on (t order key, pair index)
@@ -441,7 +443,7 @@ struct Work {
   uint32_t *count;   // [n]
   unsigned long long *key;  // [n]
   float *slot;       // [cap][kSlotWords] per-pair hit (AoS, 48 bytes)
-  float4 *pairs;     // [2][cap] pair records: (s.xyz, ray) and (d.xyz, patch) -- the ray travels with the pair
+  uint2 *pairs;      // [cap] pair records (ray, patch); the Newton stage reads the ray from the ray array
   uint32_t *fol;     // [cap] pair | what << 30
   uint32_t *ovf;     // [n]
   uint32_t *lanes;   // [cap / 64 + 1] chunks for k_newton_lane (count in ctr[3])
@@ -826,15 +828,15 @@ __global__ __launch_bounds__(kBlock) void k_scatter(const float *__restrict__ ra
                                                     uint32_t n, Work w) {
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
+  (void)rays;
+  (void)ld;
+  (void)off;
   uint32_t c = w.count[i];
   if (c > kMaxCand || c == 0) return;
-  f3 s, d;
-  load_ray(rays, ld, off + i, s, d);
   for (uint32_t j = 0; j < c; ++j) {
     const uint32_t b = w.cand[(size_t)j * n + i];
     const uint32_t p = w.offs[b] + w.rank[(size_t)j * n + i];
-    w.pairs[p] = make_float4(s.x, s.y, s.z, __uint_as_float(i));
-    w.pairs[(size_t)w.cap + p] = make_float4(d.x, d.y, d.z, __uint_as_float(b));
+    w.pairs[p] = make_uint2(i, b);
   }
 }
 
@@ -863,7 +865,8 @@ __device__ __forceinline__ void flush_follow(uint32_t *buf, uint32_t &nf, uint32
 #define BZR_NEWTON_ATTR __attribute__((amdgpu_waves_per_eu(BZR_NEWTON_WPE)))
 template <bool kFast>
 __global__ __launch_bounds__(kBlock) BZR_NEWTON_ATTR void k_newton(const float *__restrict__ full, const uint32_t *__restrict__ total,
-                                                   const float4 *__restrict__ pairs, float *__restrict__ slot,
+                                                   const uint2 *__restrict__ pairs, const float *__restrict__ rays,
+                                                   uint32_t ld, uint32_t off, float *__restrict__ slot,
                                                    uint32_t cap, unsigned long long *__restrict__ key,
                                                    uint32_t *__restrict__ fol, uint32_t *__restrict__ nfol,
                                                    uint32_t *__restrict__ lanes, uint32_t *__restrict__ nlanes) {
@@ -879,21 +882,16 @@ __global__ __launch_bounds__(kBlock) BZR_NEWTON_ATTR void k_newton(const float *
 #else
   uint32_t q = blockIdx.x * kWaves + (threadIdx.x >> 6);
 #endif
-  float4 a = make_float4(0.0f, 0.0f, 0.0f, 0.0f), e = a;
-  if (q < nchunks && q * 64u + lane < P) {
-    a = pairs[q * 64u + lane];
-    e = pairs[(size_t)cap + q * 64u + lane];
-  }
+  uint2 pr = make_uint2(0u, 0u);
+  if (q < nchunks && q * 64u + lane < P) pr = pairs[q * 64u + lane];
   for (; q < nchunks; q += W) {
     const uint32_t p = q * 64u + lane;
     bool todo = p < P;
-    const f3 s = mk(a.x, a.y, a.z), d = mk(e.x, e.y, e.z);
-    const uint32_t ray = __float_as_uint(a.w), b = __float_as_uint(e.w);
-    const uint32_t qn = q + W, pn = qn * 64u + lane;  // prefetch the next chunk
-    if (qn < nchunks && pn < P) {
-      a = pairs[pn];
-      e = pairs[(size_t)cap + pn];
-    }
+    const uint32_t ray = pr.x, b = pr.y;
+    f3 s = mk(0.0f, 0.0f, 0.0f), d = s;
+    if (todo) load_ray(rays, ld, off + ray, s, d);  // pairs of one patch: mostly neighbouring rays
+    const uint32_t qn = q + W, pn = qn * 64u + lane;  // prefetch the next chunk's pair records
+    if (qn < nchunks && pn < P) pr = pairs[pn];
     bool is_fol = false;
     uint32_t fol_entry = 0;
     // a chunk spanning many small buckets would take one pass per patch here: hand it to k_newton_lane
@@ -934,7 +932,8 @@ __global__ __launch_bounds__(kBlock) BZR_NEWTON_ATTR void k_newton(const float *
 // pair with its own patch record in VGPRs, so a fragmented chunk costs one pass instead of one per patch.
 template <bool kFast>
 __global__ __launch_bounds__(kBlock) void k_newton_lane(const float *__restrict__ full, const uint32_t *__restrict__ total,
-                                                        const float4 *__restrict__ pairs, float *__restrict__ slot,
+                                                        const uint2 *__restrict__ pairs, const float *__restrict__ rays,
+                                                        uint32_t ld, uint32_t off, float *__restrict__ slot,
                                                         uint32_t cap, unsigned long long *__restrict__ key,
                                                         uint32_t *__restrict__ fol, uint32_t *__restrict__ nfol,
                                                         const uint32_t *__restrict__ lanes,
@@ -947,11 +946,13 @@ __global__ __launch_bounds__(kBlock) void k_newton_lane(const float *__restrict_
     bool is_fol = false;
     uint32_t fol_entry = 0;
     if (p < P) {
-      const float4 a = pairs[p], e = pairs[(size_t)cap + p];
-      const uint32_t b = __float_as_uint(e.w);
+      const uint2 pr = pairs[p];
+      const uint32_t b = pr.y;
+      f3 s, d;
+      load_ray(rays, ld, off + pr.x, s, d);
       const Patch pa = load_patch(full + (size_t)rec::kWords * b);
-      const Hit h = patch_intersect<BZR_NEWTON_GATED != 0, kFast>(pa, mk(a.x, a.y, a.z), mk(e.x, e.y, e.z), false);
-      if (h.what == kIntersect) record(slot, cap, p, h, b, &key[__float_as_uint(a.w)]);
+      const Hit h = patch_intersect<BZR_NEWTON_GATED != 0, kFast>(pa, s, d, false);
+      if (h.what == kIntersect) record(slot, cap, p, h, b, &key[pr.x]);
       is_fol = h.what <= kFollow2;
       fol_entry = p | (h.what << 30);
     }
@@ -1023,12 +1024,13 @@ __global__ __launch_bounds__(kBlock) void k_resolve(MeshView m, const float *__r
   const uint32_t F = __builtin_amdgcn_readfirstlane(w.ctr[0]);
   for (uint32_t q = blockIdx.x * kBlock + threadIdx.x; q < F; q += gridDim.x * kBlock) {
     const uint32_t f = w.fol[q], p = f & 0x3FFFFFFFu, what = f >> 30;
-    const float4 a = w.pairs[p], e = w.pairs[(size_t)w.cap + p];
-    const f3 s = mk(a.x, a.y, a.z), d = mk(e.x, e.y, e.z);
-    const uint32_t nbr = __float_as_uint(m.full[(size_t)rec::kWords * __float_as_uint(e.w) + rec::kNeigh + what]);
+    const uint2 pr = w.pairs[p];
+    f3 s, d;
+    load_ray(rays, ld, off + pr.x, s, d);
+    const uint32_t nbr = __float_as_uint(m.full[(size_t)rec::kWords * pr.y + rec::kNeigh + what]);
     Patch pa = load_patch(m.full + (size_t)rec::kWords * nbr);
     Hit h = patch_intersect<false, kFast>(pa, s, d, true);
-    if (h.what == kIntersect) record(w.slot, w.cap, p, h, nbr, &w.key[__float_as_uint(a.w)]);
+    if (h.what == kIntersect) record(w.slot, w.cap, p, h, nbr, &w.key[pr.x]);
   }
   const uint32_t V = __builtin_amdgcn_readfirstlane(w.ctr[1]);
   const uint32_t S = (m.n + kOvfSlice - 1) / kOvfSlice;
@@ -1803,7 +1805,7 @@ bzr_status ensure_work(bzr_ctx *ctx, uint32_t chunk, uint32_t nb, Work &w) {
   const size_t cap = (size_t)kMaxCand * chunk;
   const size_t bytes = round256(32) + round256((size_t)(hn + 1) * 4) + round256((size_t)(hn + 1) * 4) + 2 * round256(cap * 4) +
                        round256((size_t)chunk * 4) + round256((size_t)chunk * 8) + round256(kSlotWords * cap * 4) +
-                       round256(cap * 32) + round256(cap * 4) + round256((size_t)chunk * 4) + round256((cap / 64 + 1) * 4) +
+                       round256(cap * 8) + round256(cap * 4) + round256((size_t)chunk * 4) + round256((cap / 64 + 1) * 4) +
                        round256(cub_bytes);
   const size_t had = ctx->work_bytes;
   if (bzr_status s = ensure_buffer(ctx->work, ctx->work_bytes, bytes)) return s;
@@ -1817,7 +1819,7 @@ bzr_status ensure_work(bzr_ctx *ctx, uint32_t chunk, uint32_t nb, Work &w) {
   w.count = st.take<uint32_t>(chunk);
   w.key = st.take<unsigned long long>(chunk);
   w.slot = st.take<float>(kSlotWords * cap);
-  w.pairs = st.take<float4>(2 * cap);
+  w.pairs = st.take<uint2>(cap);
   w.fol = st.take<uint32_t>(cap);
   w.ovf = st.take<uint32_t>(chunk);
   w.lanes = st.take<uint32_t>(cap / 64 + 1);
@@ -1827,8 +1829,8 @@ bzr_status ensure_work(bzr_ctx *ctx, uint32_t chunk, uint32_t nb, Work &w) {
   return BZR_OK;
 }
 
-// Rays per chunk of the staged path, whose workspace is ~3.7 KB per ray: at most
-// 2^BZR_CHUNK_LOG2 (8M rays, ~31 GB) and at most what a quarter of the device's free memory holds (at the
+// Rays per chunk of the staged path, whose workspace is ~2.7 KB per ray: at most
+// 2^BZR_CHUNK_LOG2 (8M rays, ~23 GB) and at most what a quarter of the device's free memory holds (at the
 // context's first staged call), with the
 // batch split into equal chunks (rounded to whole waves).  Measured on cfg5 (67M rays): 1M-ray chunks
 // 28.3 ms per frame, 4M 21.4, 8M 20.0, 16M 20.0 -- small chunks leave the kernels short of waves.
@@ -1836,7 +1838,7 @@ bzr_status ensure_work(bzr_ctx *ctx, uint32_t chunk, uint32_t nb, Work &w) {
 #define BZR_CHUNK_LOG2 23
 #endif
 constexpr uint32_t kChunk = 1u << BZR_CHUNK_LOG2;
-constexpr size_t kWorkBytesPerRay = (size_t)kMaxCand * (4 + 4 + 48 + 32 + 4) + 16;
+constexpr size_t kWorkBytesPerRay = (size_t)kMaxCand * (4 + 4 + 48 + 8 + 4) + 16;
 uint32_t chunk_for(bzr_ctx *ctx, uint64_t n) {
   if (!ctx->chunk_cap) {
     size_t free_b = 0, total_b = 0;
@@ -1874,10 +1876,10 @@ bzr_status run_culled(bzr_ctx *ctx, const MeshView &mv, const float *rays, uint3
   // persistent grid: the resident capacity of the device, never more than the worst-case chunk count
   const uint32_t gn = std::min<uint32_t>(std::max<uint32_t>((kMaxCand * n + kBlock - 1) / kBlock, 1u),
                                          resident_blocks(ctx, k_newton<kFast>));
-  launch(ctx, BZR_KERNEL_NEWTON, k_newton<kFast>, dim3(gn), mv.full, w.offs + hn, w.pairs, w.slot, w.cap, w.key, w.fol,
+  launch(ctx, BZR_KERNEL_NEWTON, k_newton<kFast>, dim3(gn), mv.full, w.offs + hn, w.pairs, rays, ld, off, w.slot, w.cap, w.key, w.fol,
          w.ctr, w.lanes, w.ctr + 3);
   launch(ctx, BZR_KERNEL_NEWTON_LANE, k_newton_lane<kFast>, dim3(std::min<uint32_t>(std::max<uint32_t>(n / 1024u, 1u), 1024u)),
-         mv.full, w.offs + hn, w.pairs, w.slot, w.cap, w.key, w.fol, w.ctr, w.lanes, w.ctr + 3);
+         mv.full, w.offs + hn, w.pairs, rays, ld, off, w.slot, w.cap, w.key, w.fol, w.ctr, w.lanes, w.ctr + 3);
   {  // follow retries + overflow rays (whose keys the Newton stage left untouched: their lists are empty)
     const uint64_t items = (uint64_t)n * ((nb + kOvfSlice - 1) / kOvfSlice);
     const uint32_t grid = std::max(std::min<uint32_t>(grid_for(n / 8 + 1), 1024u),

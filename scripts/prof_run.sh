@@ -19,5 +19,5 @@ run write --pmc WRITE_SIZE --kernel-trace &&
 run sq1 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU --kernel-trace &&
 run sq2 --pmc SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_SMEM SQ_INSTS_LDS SQ_LEVEL_WAVES --kernel-trace &&
 timeout -k 10 120 python3 "$R/scripts/prof_summary.py" "$OUT" "$OUT/summary.txt" --note "rocprofv3 over bench.py ${BENCH:-} (steps ${STEPS:-5})" \
-  --traffic-json "$OUT/pmc_traffic.json" --workload "${WORKLOAD:-$TAG}" > /dev/null &&
+  --traffic-json "$OUT/pmc_traffic.json" --workload "${WORKLOAD:-$TAG}" --source "profiles/${TAG:-prof}.txt" > /dev/null &&
 find "$OUT" -name "*.db" -delete

@@ -146,6 +146,7 @@ def main():
     ap.add_argument("--note", default="")
     ap.add_argument("--traffic-json", default=None)
     ap.add_argument("--workload", default=None)
+    ap.add_argument("--source", default=None, help="path recorded as the workload's source (the committed copy)")
     a = ap.parse_args()
     lines = [a.note, ""] if a.note else []
     lines += trace_section(f"{a.rundir}/trace")
@@ -154,7 +155,7 @@ def main():
     Path(a.out).write_text("\n".join(lines) + "\n")
     print("\n".join(lines))
     if a.traffic_json:
-        write_traffic(p, a.out, a.traffic_json, a.workload)
+        write_traffic(p, a.source or a.out, a.traffic_json, a.workload)
 
 
 if __name__ == "__main__":
