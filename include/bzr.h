@@ -41,6 +41,11 @@
  *     where each patch's planar gate can pass, and only those patches reach
  *     the Newton stage -- the output bits are the brute-force scan's.
  *     BZR_ACCEL_NONE runs the reference's brute-force scan itself (A/B testing).
+ *     Patches with no proven bound on where their float gate can pass (planes
+ *     through ~the origin whose M is rounding-dominated, non-finite records)
+ *     are not in the BVH: every wave tests them (the always list).
+ *   - Flags are checked first: unknown bits, BZR_PIPELINE_STAGED together with
+ *     BZR_PIPELINE_FUSED, or FAST | ACCEL_NONE return BZR_ERR_INVALID_ARGUMENT.
  */
 #ifndef BZR_H
 #define BZR_H

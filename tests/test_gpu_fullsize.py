@@ -103,3 +103,30 @@ def test_full_frame_matches_oracle_digests(bzr, ctx, lenses, pipe, name):
                            f"{ref['hits'][bad[:8]].tolist()})")
     assert np.array_equal(hits, ref["hits"])
     assert hits.sum() > 0
+
+
+def test_always_list_batches_and_open_wedges(bzr, ctx, lenses):
+    """A cfg2 lens whose 100 random patches get a non-finite barycentric inverse (no proven gate region:
+    they go to the always list, two 64-patch bundle batches, open wedges) and whose other patches keep
+    theirs: both culled pipelines == brute force on grid rays and on rays from everywhere."""
+    p = lenses("cfg2")[0].copy()
+    rng = np.random.default_rng(77)
+    bad = rng.choice(len(p), 100, replace=False)
+    p[bad[:50], 49] = np.nan
+    p[bad[50:], 53] = np.inf
+    dm = bzr.DeviceMesh(ctx, p)
+    from bzr_amd.configs import grid_rays
+    rays = grid_rays(CONFIGS["cfg2"], side=256)
+    n = 65536
+    o = rng.uniform(-20, 30, (n, 3))
+    tgt = np.array([10.0, 0.0, 0.0]) + rng.uniform(-1, 1, (n, 3)) * np.array([1.0, 4.0, 2.0])
+    d = (tgt - o) / np.linalg.norm(tgt - o, axis=1, keepdims=True)
+    rays = np.concatenate([rays, np.concatenate([o.T, d.T]).astype(np.float32)], axis=1)
+    want = _bits(bzr.intersect(ctx, dm, rays, mode=bzr.ACCEL_NONE))
+    for pipe in (bzr.PIPELINE_FUSED, bzr.PIPELINE_STAGED):
+        assert np.array_equal(_bits(bzr.intersect(ctx, dm, rays, mode=pipe)), want), pipe
+        got = bzr.trace_chain(ctx, [dm], [1.3], rays[:, :65536], mode=pipe)
+        ref = bzr.trace_chain(ctx, [dm], [1.3], rays[:, :65536], mode=bzr.ACCEL_NONE)
+        for x, y in zip(got, ref):
+            assert np.array_equal(_bits(x), _bits(y)), pipe
+    assert (want[11] == 4).mean() > 0.05
