@@ -77,8 +77,8 @@ BYTES_INTERSECT = 24 + 52     # per ray: ray in; BezierIntersection (13 words) o
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--steps", type=int, default=100)
+    p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--config", default="cfg4", choices=["cfg2", "cfg3", "cfg4", "cfg5"])
     p.add_argument("--side", type=int, default=0, help="override rays per image side")
     p.add_argument("--scaling", default="strong", choices=["strong", "weak"])

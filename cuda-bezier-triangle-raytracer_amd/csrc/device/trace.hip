@@ -1140,6 +1140,10 @@ struct TraceCtr {  // wave-uniform work counters (kCount)
 #ifndef BZR_TRACE_SPEC
 #define BZR_TRACE_SPEC 1
 #endif
+// BZR_TRACE_PARK_HITS (A/B knob): park cNone results in the intersect kernel (kModeHits) as well.
+#ifndef BZR_TRACE_PARK_HITS
+#define BZR_TRACE_PARK_HITS 0
+#endif
 constexpr uint32_t kEntries = BZR_TRACE_ENTRIES;  // collected leaves per batch: power of two, <= 64
 static_assert(kEntries >= 4 && kEntries <= 64 && (kEntries & (kEntries - 1)) == 0, "kEntries");
 // Words kept per lane: the winner (all of BezierIntersection for kModeHits; what refraction reads
@@ -1147,7 +1151,9 @@ static_assert(kEntries >= 4 && kEntries <= 64 && (kEntries & (kEntries - 1)) == 
 template <int kMode>
 struct TraceWords {
   static constexpr int kHit = kMode == kModeHits ? 12 : 7;
-  static constexpr int kPark = (kMode != kModeHits && BZR_TRACE_SPEC) ? 8 : 0;
+  // kModeHits parks the barycentrics too (11 words): 6.4 KB of LDS per wave, which its 6 waves per SIMD
+  // (80 VGPRs) leave room for (24 waves x 6.4 KB <= 160 KB)
+  static constexpr int kPark = !BZR_TRACE_SPEC ? 0 : (kMode != kModeHits ? 8 : (BZR_TRACE_PARK_HITS ? 11 : 0));
 };
 template <int kMode>
 struct TraceLds {  // per wave
@@ -1234,6 +1240,11 @@ __device__ __forceinline__ void park(const Hit &h, TraceLds<kMode> &L, uint32_t 
     L.park[5][lane] = h.normal.x;
     L.park[6][lane] = h.normal.y;
     L.park[7][lane] = h.normal.z;
+    if constexpr (TraceWords<kMode>::kPark >= 11) {  // kModeHits: the whole BezierIntersection
+      L.park[8][lane] = h.bary.x;
+      L.park[9][lane] = h.bary.y;
+      L.park[10][lane] = h.bary.z;
+    }
   }
 }
 template <int kMode>
@@ -1244,6 +1255,7 @@ __device__ __forceinline__ Hit parked(TraceLds<kMode> &L, uint32_t lane) {
     h.point = mk(L.park[1][lane], L.park[2][lane], L.park[3][lane]);
     h.cs = L.park[4][lane];
     h.normal = mk(L.park[5][lane], L.park[6][lane], L.park[7][lane]);
+    if constexpr (TraceWords<kMode>::kPark >= 11) h.bary = mk(L.park[8][lane], L.park[9][lane], L.park[10][lane]);
     h.what = kIntersect;
   }
   return h;
