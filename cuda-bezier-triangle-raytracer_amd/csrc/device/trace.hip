@@ -1140,9 +1140,10 @@ struct TraceCtr {  // wave-uniform work counters (kCount)
 #ifndef BZR_TRACE_SPEC
 #define BZR_TRACE_SPEC 1
 #endif
-// BZR_TRACE_PARK_HITS (A/B knob): park cNone results in the intersect kernel (kModeHits) as well.
+// BZR_TRACE_PARK_HITS (default 1): park cNone results in the intersect kernel (kModeHits) as well: cfg5
+// fused -7.8 % Newton passes, +3.2 % Mrays/s; cfg3 +1 % (profiles/r03_ab_cfg{5,3}_fused_parkhits.jsonl).
 #ifndef BZR_TRACE_PARK_HITS
-#define BZR_TRACE_PARK_HITS 0
+#define BZR_TRACE_PARK_HITS 1
 #endif
 constexpr uint32_t kEntries = BZR_TRACE_ENTRIES;  // collected leaves per batch: power of two, <= 64
 static_assert(kEntries >= 4 && kEntries <= 64 && (kEntries & (kEntries - 1)) == 0, "kEntries");
