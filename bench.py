@@ -338,15 +338,19 @@ def main():
     # steps start at the clock the chip holds under this load (scripts/sustained_clock.py: the first
     # ~0.2 s of frames run ~3 % slower); then the W warmup steps, right before the timed ones (no host
     # round trip in between)
+    # (tracing only: no gather, so ranks may run different frame counts without a collective mismatch)
     if a.prewarm_s > 0:
-        t_pw = time.perf_counter()
+        t_pw, k_pw = time.perf_counter(), 0
         while True:
             for _ in range(8):
-                step()
-            drain()
+                with torch.cuda.stream(streams[k_pw % F]):
+                    trace(k_pw % F, k_pw)
+                k_pw += 1
             torch.cuda.synchronize()
             if time.perf_counter() - t_pw >= a.prewarm_s:
                 break
+        if world > 1:
+            dist.barrier()
     for _ in range(a.warmup):
         step()
     drain()
