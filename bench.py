@@ -316,10 +316,12 @@ def main():
     # (strong scaling may deal one tile fewer to some ranks).  Layouts: rays (chain: 6 ray rows + the
     # status/segment word; intersect: the 13 hit rows), compact (every final ray, survivors only), image
     # (one word per primary; intersect: the hit's `what` row).
-    pack_fn = None
-    if not chain:
-        pack_fn = ((lambda out, p: p[0, :n].copy_(out[11])) if a.gather == "image" else
-                   (lambda out, p: p[:, :n].copy_(out)))
+    # chain frames are packed on the device by bzr_pack_frame (one kernel; three for compact) on the slot's context
+    if chain:
+        pack_fn = lambda out, p, f: bzr_amd.pack_frame(ctxs[f], a.gather, *out, p, npad, cap)  # noqa: E731
+    else:
+        pack_fn = ((lambda out, p, f: p[0, :n].copy_(out[11])) if a.gather == "image" else
+                   (lambda out, p, f: p[:, :n].copy_(out)))
     loop = frame.FrameLoop(world, rank, n, npad, a.gather, trace, outs, stream_for=lambda f: torch.cuda.stream(streams[f]),
                            cap=cap, device=dev, pack_fn=pack_fn, rows=0 if chain else 13)
 

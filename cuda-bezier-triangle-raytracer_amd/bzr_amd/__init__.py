@@ -98,6 +98,7 @@ _SIGS = {
     "bzr_bezier_build": [_P, _P],
     "bzr_bezier_split_thick": [_P, _P],
     "bzr_bezier_interpolate": [_P, _I32, _P],
+    "bzr_pack_frame": [_P, _I32, _P, _P, _P, _U32, _U32, _U32, _P],
     "bzr_debug_unit": [_P, _P, _U32, _P],
     "bzr_debug_wave_clock": [_P, _P, _U32],
     "bzr_debug_wave_clock_rate": [_P, _P, _U32],
@@ -362,6 +363,29 @@ def trace_chain(ctx: Context, lenses, ri, rays, out_rays=None, out_status=None, 
         _check(lib().bzr_trace_chain(ctx.handle, ctypes.cast(handles, _P), ctypes.cast(ris, _P), nl, r.ptr, n, o.ptr,
                                      s.ptr, g.ptr, res | mode))
     return out_rays, out_status, out_segments
+
+
+PACK_IMAGE, PACK_RAYS, PACK_COMPACT = 0, 1, 2  # BZR_PACK_*
+PACK_LAYOUTS = {"image": PACK_IMAGE, "rays": PACK_RAYS, "compact": PACK_COMPACT}
+
+
+def pack_frame(ctx: Context, layout: str, rays, status, segments, packed, npad: int, cap: int = 0):
+    """bzr_pack_frame: one chain frame's device outputs (rays [6, n], status [n], segments [n]) into the
+    gather buffer `packed` (a CUDA tensor laid out as bzr_amd.frame's `layout`: image, rays or compact)
+    on the device, no host sync.  Same bits as frame.pack / frame.pack_compact in the columns they read."""
+    if layout not in PACK_LAYOUTS:
+        raise ValueError(f"layout {layout!r}")
+    n = int(status.shape[0])
+    bufs = [_Buf(status, np.uint32), _Buf(segments, np.uint32), _Buf(packed, np.float32, True)]
+    r = _Buf(rays, np.float32) if rays is not None else _Buf(None, np.float32)
+    if r.ptr is not None:
+        bufs.append(r)
+    if _residency(*bufs) != DEVICE_PTRS:
+        raise BzrError("pack_frame takes device tensors")
+    with _stream_for(ctx, DEVICE_PTRS):
+        _check(lib().bzr_pack_frame(ctx.handle, PACK_LAYOUTS[layout], r.ptr, bufs[0].ptr, bufs[1].ptr, n, int(npad),
+                                    int(cap), bufs[2].ptr))
+    return packed
 
 
 def trace_tiled(ctxs, lenses, ri, rays, tile_rays=4096, mode=MODE_PARITY):

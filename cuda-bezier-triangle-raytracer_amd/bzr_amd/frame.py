@@ -169,10 +169,13 @@ class FrameLoop:
     CPU).  With a gather layout the frame is then packed into gather buffer k % 2 -- after that buffer's
     previous gather completed -- and gathered to rank 0 asynchronously, so frame k's gather overlaps
     frame k + 1's tracing.  on_gathered(frame, parts) (rank 0, optional) sees each frame's gathered
-    buffers when its handle is waited for (the next use of the buffer, or drain())."""
+    buffers when its handle is waited for (the next use of the buffer, or drain()).  pack_fn(outs[slot], packed,
+    slot), when given, packs instead of pack() / pack_compact() (bench.py: bzr_amd.pack_frame on the slot's
+    context, one HIP kernel instead of a dozen torch ops; or the intersect configs' hit rows).  pack_always packs every
+    frame even with world == 1 (no collective: scripts/rank_loop_probe.py times one rank's loop that way)."""
 
     def __init__(self, world: int, rank: int, n: int, npad: int, layout: str, trace, outs, stream_for=None,
-                 cap: int = 0, device=None, on_gathered=None, pack_fn=None, rows: int = 0):
+                 cap: int = 0, device=None, on_gathered=None, pack_fn=None, rows: int = 0, pack_always: bool = False):
         import contextlib
 
         import torch
@@ -183,7 +186,7 @@ class FrameLoop:
         self.trace, self.outs = trace, outs
         self.stream_for = stream_for or (lambda f: contextlib.nullcontext())
         self.cap, self.on_gathered, self.pack_fn = cap, on_gathered, pack_fn
-        self.gather_on = world > 1 and layout != "none"
+        self.gather_on = (world > 1 or pack_always) and layout != "none"
         self.frames = 0
         self.pending = [None, None]
         self.pending_frame = [-1, -1]
@@ -213,8 +216,8 @@ class FrameLoop:
             if self.gather_on:
                 slot = self.frames % 2
                 self._finish(slot)
-                if self.pack_fn is not None:  # other result shapes (bench.py's intersect configs)
-                    self.pack_fn(self.outs[f], self.packed[slot])
+                if self.pack_fn is not None:  # a device packer (bzr_amd.pack_frame) or other result shapes
+                    self.pack_fn(self.outs[f], self.packed[slot], f)
                 elif self.layout == "compact":
                     rays, status, seg = self.outs[f]
                     pack_compact(status, seg, rays, self.packed[slot], self.npad, self.cap)

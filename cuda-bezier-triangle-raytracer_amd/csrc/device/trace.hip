@@ -32,6 +32,7 @@
 
 #include "../host/bvh.hpp"
 #include "bzr.h"
+#include "ctx.hpp"
 #include "patch_math.hpp"
 #include "emitter.hpp"
 
@@ -75,37 +76,6 @@ struct bzr_mesh {
   float s_max;      // far tier: origins beyond take the full scan
   float s_near;     // near tier: waves whose rays all start within it walk the tighter tree
   float sphere[4];  // Ritter sphere over the gate-region boxes (bvh.cpp): the illumination pre-cull
-};
-
-struct bzr_ctx {
-  int device;
-  hipStream_t own;
-  hipStream_t stream;
-  void *scratch = nullptr;  // staging for host-pointer calls
-  size_t scratch_bytes = 0;
-  void *work = nullptr;     // candidate lists + counts
-  size_t work_bytes = 0;
-  // The culled path's counters and histogram start every segment at zero.  A segment on the small-scan
-  // path leaves them zero for the next one (k_scan_small clears the histogram it reads, k_finish the
-  // counters), so the memset is skipped while the workspace and histogram size are unchanged.
-  const uint32_t *zero_ctr = nullptr;  // workspace counters known zero, with histogram [0, zero_hn]
-  uint32_t zero_hn = 0;
-  bool timing = false;      // per-kernel event timing (bzr_ctx_timing)
-  struct Mark {
-    int kernel;
-    hipEvent_t start, stop;
-  };
-  std::vector<Mark> marks;       // recorded, not yet reported
-  std::vector<hipEvent_t> spare; // event pool
-  hipEvent_t handoff = nullptr;  // orders a new stream after the previous one (bzr_ctx_set_stream)
-  double ms[BZR_KERNEL_COUNT] = {};
-  uint32_t calls[BZR_KERNEL_COUNT] = {};
-  uint32_t chunk_cap = 0;                // staged-path rays per chunk (0: not yet sized, chunk_for)
-  bool counting = false;                 // work counters (bzr_ctx_counters)
-  unsigned long long *counters = nullptr;  // device [BZR_COUNTER_COUNT]
-  unsigned long long *wave_clock = nullptr;  // test hook (bzr_debug_wave_clock): per k_trace wave, device
-  uint32_t wave_clock_cap = 0;
-  bool wave_clock_real = false;  // bzr_debug_wave_clock_rate: also s_memrealtime (4 words per wave)
 };
 
 namespace {
@@ -2054,6 +2024,7 @@ extern "C" bzr_status bzr_ctx_destroy(bzr_ctx *ctx) {
   if (ctx->scratch) (void)hipFree(ctx->scratch);
   if (ctx->work) (void)hipFree(ctx->work);
   if (ctx->counters) (void)hipFree(ctx->counters);
+  if (ctx->pack) (void)hipFree(ctx->pack);
   (void)hipStreamDestroy(ctx->own);
   delete ctx;
   return BZR_OK;

@@ -251,6 +251,26 @@ bzr_status bzr_illuminate(bzr_ctx *ctx, const bzr_mesh *const *lenses, const flo
 /* The bounding sphere bzr_illuminate culls with: center xyz, radius. */
 bzr_status bzr_mesh_bounding_sphere(const bzr_mesh *mesh, float out[4]);
 
+/* ---- multi-GPU frames: a rank's results into its gather buffer (bzr_amd/frame.py) ---- */
+/* No reference counterpart: the reference is single-process (its refraction chain loop,
+ * reference/test.cpp:376-401, keeps the results in host vectors); this is the step between
+ * bzr_trace_chain and the per-frame gather of a sharded image. */
+enum { BZR_PACK_IMAGE = 0, BZR_PACK_RAYS = 1, BZR_PACK_COMPACT = 2 };
+/* One chain frame's outputs (bzr_trace_chain: rays_soa [6][n], status [n], segments [n]; device
+ * pointers) into `packed` (device) on the context's stream, without a host sync.  npad >= n is the
+ * padded per-rank column count of the gather buffer.
+ *   BZR_PACK_IMAGE    packed[npad] words: word i = status | segments << 8 (rays_soa may be NULL)
+ *   BZR_PACK_RAYS     packed[7][npad]: the 6 ray rows, then the word row
+ *   BZR_PACK_COMPACT  npad / 4 words of bytes, byte i = (status & 3) | segments << 2; then the
+ *                     survivor count (uint32); then 6 rows of cap + 1 floats holding the rays of the
+ *                     survivors (segments >= 2 or status != 0) in ray order.  0 < cap <= npad, npad a
+ *                     multiple of 4; survivors past cap are counted but not written (the reader checks
+ *                     count <= cap).
+ * Columns >= n (and the last column of each compact row) are not written.  With n = 0 the input
+ * pointers may be NULL. */
+bzr_status bzr_pack_frame(bzr_ctx *ctx, int32_t layout, const float *rays_soa, const uint32_t *status,
+                          const uint32_t *segments, uint32_t n, uint32_t npad, uint32_t cap, void *packed);
+
 /* ---- host preprocessing (reference Mesh / BezierMesh construction) ---- */
 enum { BZR_ENVELOPE_ELLIPSOID = 0, BZR_ENVELOPE_TESTLENS = 1 };
 bzr_status bzr_trimesh_create(bzr_trimesh **out);

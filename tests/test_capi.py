@@ -100,3 +100,23 @@ def test_patch_records_view_as_reference_struct(bzr):
     assert neigh.max() < len(p)
     assert np.array_equal(p[:, 60:63], np.tile([1.0, 0.0, -1.0], (len(p), 1)).astype(np.float32))
     assert (p[:, 58] <= 0).all() and (p[:, 59] >= 0).all()  # mHeightInside <= 0 <= mHeightOutside
+
+
+def test_pack_frame_validates_before_touching_a_device(bzr):
+    """bzr_pack_frame (the gather-buffer packer, include/bzr.h) rejects bad layouts and sizes before it
+    looks at the context."""
+    L = bzr.lib()
+    p = ctypes.c_void_p(16)  # never dereferenced: every call below fails validation first
+    cases = [((7, p, p, p, 10, 16, 0, p), b"unknown pack layout"),
+             ((bzr.PACK_IMAGE, None, p, p, 17, 16, 0, p), b"n > npad"),
+             ((bzr.PACK_COMPACT, p, p, p, 10, 18, 4, p), b"multiple of 4"),
+             ((bzr.PACK_COMPACT, p, p, p, 10, 16, 0, p), b"0 < cap"),
+             ((bzr.PACK_COMPACT, p, p, p, 10, 16, 17, p), b"0 < cap"),
+             ((bzr.PACK_RAYS, None, p, p, 10, 16, 0, p), b"null rays"),
+             ((bzr.PACK_IMAGE, None, None, p, 10, 16, 0, p), b"null status"),
+             ((bzr.PACK_IMAGE, None, p, p, 10, 16, 0, None), b"null status"),
+             ((bzr.PACK_COMPACT, None, None, None, 0, 16, 4, p), b"null context"),  # n = 0: empty inputs
+             ((bzr.PACK_IMAGE, None, p, p, 10, 16, 0, p), b"null context")]
+    for args, msg in cases:
+        assert L.bzr_pack_frame(None, *args) == 1, args
+        assert msg in L.bzr_last_error(), (args, L.bzr_last_error())
