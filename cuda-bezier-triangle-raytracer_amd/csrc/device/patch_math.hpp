@@ -120,6 +120,10 @@ struct Hit {
 #define BZR_NEWTON_UNROLL 1
 #endif
 constexpr uint32_t kFollow2 = 2u, kNone = 3u, kIntersect = 4u;
+// BZR_PASS_FLAT (default 0): patch_intersect's gate without the early return (see there).
+#ifndef BZR_PASS_FLAT
+#define BZR_PASS_FLAT 0
+#endif
 
 // Correctly rounded binary32 division and square root.  HIP compiles `/` and
 // __builtin_sqrtf correctly rounded by default (-fhip-fp32-correctly-rounded-divide-sqrt);
@@ -225,6 +229,20 @@ __device__ __forceinline__ Hit patch_intersect(const P &p, f3 s, f3 d, bool limi
   float ic, it;
   bool valid = plane_ray(p.n(), p.c(), s, d, ip, ic, it);
   (void)valid;
+#if BZR_PASS_FLAT
+  if (!kGated) {
+    // Branch-free form: every lane of the call runs the Newton tail and lanes whose gate fails get the
+    // kNone record afterwards -- the same bits for the lanes that pass, and no divergent branch, so the
+    // record's scalar loads need not wait inside one (they batch ahead of the arithmetic).
+    const f3 b0 = matvec(p, ip);
+    const bool in = (b0.x >= 0.0f) & (b0.x <= 1.0f) & (b0.y >= 0.0f) & (b0.y <= 1.0f) & (b0.z >= 0.0f) & (b0.z <= 1.0f);
+    const bool ok = valid & (fabsf(it) > -p.hin()) & (fabsf(it) > p.hout()) & (limitNone | in);
+    Hit r;
+    if constexpr (kFast) r = fast::newton_tail(p, s, d, ic, it);
+    else r = newton_tail(p, s, d, ic, it);
+    return ok ? r : h;
+  }
+#endif
   if (!kGated) {
     if (!(valid && fabsf(it) > -p.hin() && fabsf(it) > p.hout())) return h;
     f3 b0 = matvec(p, ip);

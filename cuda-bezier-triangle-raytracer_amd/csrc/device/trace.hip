@@ -69,6 +69,8 @@ struct bzr_mesh {
   float4 *leaf_near;
   bzr_host::Bvh4ObbNode *obb;       // both tiers' wide-patch subtrees (oriented boxes, bvh.hpp)
   bzr_host::Bvh4ObbNode *obb_near;
+  float4 *kids;      // the far tree's children AoS (2 float4 per child: lo.xyz ref, hi.xyz 0): the bundle walk's
+  float4 *kids_near; // per-lane child records (kids_of), and the near tree's
   float4 *always;   // 8 float4 per always-tested patch (bvh.hpp Bvh::always): planar record with the patch index
                     // in its last word, then the wedge pre-test (always_wedge: w.xyz L H B C 0) and 8 pad words
   uint32_t n_always;
@@ -137,6 +139,19 @@ constexpr int kTravBlock = BZR_TRAV_BLOCK;
 #endif
 // BZR_NEWTON_XCD (default 0): k_newton waves take chunks in XCD-contiguous order (measured +6 %, off).
 // BZR_GATE_FLAT (default 1): planar_gate without early-out branches (see there).
+// BZR_NODE_ASM (default 0): fetch a BVH node's two halves with one inline-asm pair of scalar loads and
+// a single wait (node_children).
+#ifndef BZR_NODE_ASM
+#define BZR_NODE_ASM 0
+#endif
+// BZR_BUNDLE_DPP (default 1): the bundle walk's ray bundle from DPP reductions (bundle_setup_dpp).
+#ifndef BZR_BUNDLE_DPP
+#define BZR_BUNDLE_DPP 1
+#endif
+// BZR_TRAV_BUNDLE (default 0): k_traverse walks with the wave-bundle test in batches (traverse_rays).
+#ifndef BZR_TRAV_BUNDLE
+#define BZR_TRAV_BUNDLE 0
+#endif
 #ifndef BZR_GATE_FLAT
 #define BZR_GATE_FLAT 1
 #endif
@@ -166,6 +181,8 @@ struct MeshView {
   const bzr_host::Bvh4ObbNode *__restrict__ obb;
   const bzr_host::Bvh4ObbNode *__restrict__ obb_near;
   const float4 *__restrict__ always;  // patches without a proven gate region: gate-tested by every wave-segment
+  const float4 *__restrict__ kids;       // AoS child records of nodes / nodes_near (bzr_mesh)
+  const float4 *__restrict__ kids_near;
   uint32_t n_always;
   uint32_t n;
   float s_max;
@@ -311,6 +328,13 @@ __device__ __forceinline__ void store_ray(float *__restrict__ r, uint32_t n, uin
   r[(size_t)5 * n + i] = d.z;
 }
 
+// Diagnostic builds (BZR_DIAG_WALK2 / BZR_DIAG_NEWTON2): a copy of a value the compiler cannot see through,
+// so a phase evaluated twice is not folded -- the marginal cost of its arithmetic, with identical results.
+__device__ __forceinline__ f3 opaque(f3 v) {
+  asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z));
+  return v;
+}
+
 // ------------------------------------------------------------ culled path
 __device__ __forceinline__ float safe_inv(float x) {
   // slab test only (no parity requirement): keep 1/d finite so (b - o) * inv never makes 0 * inf
@@ -376,7 +400,19 @@ __device__ __forceinline__ void node_children(const bzr_host::Bvh4Node *nodes, c
   }
   // the whole 128-byte node in two 64-byte scalar loads and one wait (all words used unconditionally)
   const cu32x16 *np = (const cu32x16 *)(uintptr_t)(nodes + ref);
+#if BZR_NODE_ASM
+  // Both loads issued back to back, then one wait.  Left to the compiler, k_trace's walk got a wait
+  // between the two (a scalar load's destination may still have a write pending from the previous
+  // iteration's leaf load on some path, and scalar loads return out of order, so the second load waited
+  // for everything): two L2 round trips per node.  Early-clobber outputs: the first load must not
+  // overwrite the address pair the second one reads.
+  u32x16 na, nb;
+  asm volatile("s_load_dwordx16 %0, %2, 0x0\n\ts_load_dwordx16 %1, %2, 0x40\n\ts_waitcnt lgkmcnt(0)"
+               : "=&s"(na), "=&s"(nb)
+               : "s"(np));
+#else
   const u32x16 na = np[0], nb = np[1];
+#endif
   // words: lo.x[0..3] lo.y lo.z hi.x | hi.y hi.z child[0..3] pad
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
@@ -384,6 +420,9 @@ __device__ __forceinline__ void node_children(const bzr_host::Bvh4Node *nodes, c
     const float4 hi = make_float4(__uint_as_float(na[12 + c]), __uint_as_float(nb[c]), __uint_as_float(nb[4 + c]), 0.0f);
     ch[c] = nb[8 + c];
     hit[c] = act & (ch[c] != bzr_host::kEmptyChild) & slab(lo, hi, s, sinv, inv);
+#if BZR_DIAG_WALK2
+    hit[c] &= slab(lo, hi, s, opaque(sinv), opaque(inv));
+#endif
   }
 }
 
@@ -462,6 +501,7 @@ __device__ __forceinline__ uint32_t t_order(float t) {
 }
 
 // Number of lanes below this one in `mask`.
+__device__ __forceinline__ uint32_t popc64_(unsigned long long m) { return (uint32_t)__popcll(m); }
 __device__ __forceinline__ uint32_t lanes_below(unsigned long long mask) {
   return __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(mask >> 32),
                                    __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(mask), 0u));
@@ -563,8 +603,8 @@ __device__ __forceinline__ float wave_maxf(float v) {
 }
 // The 12 reductions one after another (a loop that is not unrolled), each stored to the wave's LDS words as
 // soon as it is done, so only one is in registers at a time; word 12 = 1 when every box bound is finite
-// (false also for an empty bundle, whose boxes are +-inf).
-constexpr uint32_t kBundleWords = 13;
+// (false also for an empty bundle, whose boxes are +-inf).  Words 13..21: bundle_derive.
+constexpr uint32_t kBundleWords = 22;
 __device__ __forceinline__ void bundle_to_lds(bool act, f3 s, f3 d, float *out, uint32_t lane) {
   const float inf = __builtin_inff();
   float m = 0.0f;
@@ -580,6 +620,130 @@ __device__ __forceinline__ void bundle_to_lds(bool act, f3 s, f3 d, float *out, 
   }
   if (lane == 0u) out[12] = m <= 1e30f ? 1.0f : 0.0f;
   __builtin_amdgcn_wave_barrier();  // the words are read back by every lane of this wave
+}
+// Wave min / max with DPP row shifts and row broadcasts (no LDS round trips): lane 63 ends with the result,
+// read back as a uniform value.  Lanes shifted in from outside a row contribute the identity.
+template <bool kMax>
+__device__ __forceinline__ float wave_reduce_dpp(float v) {
+  const int id = __float_as_int(kMax ? -__builtin_inff() : __builtin_inff());
+#define BZR_DPP_STEP(ctrl, rows)                                                                        \
+  {                                                                                                    \
+    const float o = __int_as_float(__builtin_amdgcn_update_dpp(id, __float_as_int(v), ctrl, rows, 0xF, false)); \
+    v = kMax ? fmaxf(v, o) : fminf(v, o);                                                              \
+  }
+  BZR_DPP_STEP(0x111, 0xF)  // row_shr:1
+  BZR_DPP_STEP(0x112, 0xF)  // row_shr:2
+  BZR_DPP_STEP(0x114, 0xF)  // row_shr:4
+  BZR_DPP_STEP(0x118, 0xF)  // row_shr:8: lane 15 of each row holds its row's result
+  BZR_DPP_STEP(0x142, 0xA)  // row_bcast:15 into rows 1 and 3
+  BZR_DPP_STEP(0x143, 0xC)  // row_bcast:31 into rows 2 and 3: lane 63 holds the wave's result
+#undef BZR_DPP_STEP
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+// The whole bundle (words 0..21: bundle_to_lds's 13 and bundle_derive's 9) with the 12 reductions side by
+// side in DPP form, written by lane 0.
+__device__ __forceinline__ void bundle_setup_dpp(bool act, f3 s, f3 d, float *out, uint32_t lane) {
+  const float inf = __builtin_inff();
+  const float r[12] = {
+      wave_reduce_dpp<false>(act ? s.x : inf),  wave_reduce_dpp<false>(act ? s.y : inf),
+      wave_reduce_dpp<false>(act ? s.z : inf),  wave_reduce_dpp<true>(act ? s.x : -inf),
+      wave_reduce_dpp<true>(act ? s.y : -inf),  wave_reduce_dpp<true>(act ? s.z : -inf),
+      wave_reduce_dpp<false>(act ? d.x : inf),  wave_reduce_dpp<false>(act ? d.y : inf),
+      wave_reduce_dpp<false>(act ? d.z : inf),  wave_reduce_dpp<true>(act ? d.x : -inf),
+      wave_reduce_dpp<true>(act ? d.y : -inf),  wave_reduce_dpp<true>(act ? d.z : -inf)};
+  if (lane == 0u) {
+    float m = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 12; ++k) {
+      out[k] = r[k];
+      m = fmaxf(m, fabsf(r[k]));
+    }
+    out[12] = m <= 1e30f ? 1.0f : 0.0f;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      const float dl = r[6 + a], dh = r[9 + a];
+      const float lo = dl > 1e-20f ? dl : fminf(dl, -1e-20f), hi = dh < -1e-20f ? dh : fmaxf(dh, 1e-20f);
+      out[13 + a] = 1.0f / lo;
+      out[16 + a] = 1.0f / hi;
+      out[19 + a] = (lo < 0.0f && hi > 0.0f) ? 1.0f : 0.0f;
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+}
+// The bundle walk's per-axis words (13..21, lane 0 after bundle_to_lds): rl = 1 / Dl', rh = 1 / Dh' and
+// mixed = 1 when Dl' < 0 < Dh', where Dl' <= Dl and Dh' >= Dh are the direction bounds moved away from zero
+// (|D'| >= 1e-20: a wider direction box, so a superset of the rays).
+__device__ __forceinline__ void bundle_derive(float *out, uint32_t lane) {
+  if (lane == 0u) {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      const float dl = out[6 + a], dh = out[9 + a];
+      const float lo = dl > 1e-20f ? dl : fminf(dl, -1e-20f), hi = dh < -1e-20f ? dh : fmaxf(dh, 1e-20f);
+      out[13 + a] = 1.0f / lo;
+      out[16 + a] = 1.0f / hi;
+      out[19 + a] = (lo < 0.0f && hi > 0.0f) ? 1.0f : 0.0f;
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+}
+// Wave-bundle box test (the bundle walk): false only when no ray s + t d, t >= 0, with s in [Sl, Sh] and d in
+// [Dl', Dh'] (per axis, so a superset of the wave's active rays) meets the box.  On axis a the reachable
+// coordinates at time t are [Sl + t Dl', Sh + t Dh'], which meet [lo, hi] iff Sl + t Dl' <= hi and
+// Sh + t Dh' >= lo: with A = (hi - Sl) / Dl' and B = (lo - Sh) / Dh', t in [B, A] when 0 < Dl' (and B <= A
+// whenever A >= 0, so [min, max] decides alike), t in [A, B] when Dh' < 0 (same), and t >= max(A, B) when
+// the axis is mixed.  A and B carry at most ~3u relative rounding (one subtraction, the rounded reciprocal,
+// one product); the bounds are widened by 8u relative + 2^-126 before tnear <= tfar and tfar >= 0, and a
+// NaN keeps the box.  The per-lane walk's boxes are padded for the lanes' own float slab test; this test
+// is conservative against the exact rays, so it keeps every box an exact ray of the wave meets (host
+// mirror: bvh.cpp bundle_box_h, checked by tests/test_culling_conservative.py).
+__device__ __forceinline__ bool bundle_box(const float *B, float4 lo, float4 hi) {
+  float tn = -__builtin_inff(), tf = __builtin_inff();
+  const float l3[3] = {lo.x, lo.y, lo.z}, h3[3] = {hi.x, hi.y, hi.z};
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    const float A = (h3[a] - B[a]) * B[13 + a], Bq = (l3[a] - B[3 + a]) * B[16 + a];
+    const float mn = fminf(A, Bq), mx = fmaxf(A, Bq);
+    const bool mix = B[19 + a] > 0.0f;
+    tn = fmaxf(tn, mix ? mx : mn);
+    tf = fminf(tf, mix ? __builtin_inff() : mx);
+  }
+  tn -= fabsf(tn) * 0x1p-21f + 0x1p-126f;
+  tf += fabsf(tf) * 0x1p-21f + 0x1p-126f;
+  return !(B[12] > 0.0f) | (!(tn > tf) & !(tf < 0.0f));
+}
+// One batch of the bundle walk (k_trace and k_traverse): the k <= 16 axis-aligned nodes on top of the wave's
+// LDS stack `stk` (the top one is axis-aligned; an oriented-box node below it ends the batch), lane 4 q + c
+// taking node q's child c from the AoS child records `kids`.  Hit inner children are pushed, hit leaf slots
+// written to `pend` (returns how many).  Returns with `full` set when the stack could not take every hit
+// child (those subtrees are dropped: the caller sends its active lanes to the full scan).
+__device__ __forceinline__ uint32_t bundle_batch(const float4 *kids, uint32_t *stk, int &sp, uint32_t *pend,
+                                                 const float *B, uint32_t lane, bool &full, uint32_t &knodes) {
+  const uint32_t q = lane >> 2, c = lane & 3u;
+  // at most (kStack - sp) / 3 nodes (at least one), so their <= 4 children each always fit: the stack then
+  // never overflows while the tree is shallower than (kStack - 1) / 3 levels (a wide bundle degrades to
+  // the per-node depth-first order, not to the full scan)
+  const int room = (kStack - sp) / 3;
+  const uint32_t kmax = (uint32_t)(sp < 16 ? sp : 16) < (uint32_t)(room > 1 ? room : 1) ? (uint32_t)(sp < 16 ? sp : 16)
+                                                                                        : (uint32_t)(room > 1 ? room : 1);
+  const uint32_t nd = q < kmax ? stk[sp - 1 - (int)q] : 0u;
+  const unsigned long long ob = __ballot(c == 0u && q < kmax && (nd & bzr_host::kObbFlag));
+  const uint32_t k = ob ? (uint32_t)__builtin_ctzll(ob) >> 2 : kmax;
+  const bool slot = q < k;
+  const float4 *kp = kids + ((size_t)(slot ? nd : 0u) * 4u + c) * 2u;
+  const float4 lo = kp[0], hi = kp[1];
+  const uint32_t ref = __float_as_uint(lo.w);
+  const bool hit = slot && ref != bzr_host::kEmptyChild && bundle_box(B, lo, hi);
+  const bool isleaf = (ref & bzr_host::kLeafFlag) != 0u;
+  const unsigned long long lm = __ballot(hit && isleaf), im = __ballot(hit && !isleaf);
+  knodes = k;
+  sp -= (int)k;
+  const int below = (int)lanes_below(im);
+  if (hit && !isleaf && sp + below < kStack) stk[sp + below] = ref;
+  const int ni = (int)popc64_(im);
+  full = sp + ni > kStack;
+  sp = full ? kStack : sp + ni;
+  if (hit && isleaf) pend[lanes_below(lm)] = ref & ~bzr_host::kLeafFlag;
+  return popc64_(lm);
 }
 // Interval of n.x over x in [lo, hi] (n fixed).
 __device__ __forceinline__ void ivdot(f3 n, f3 lo, f3 hi, float &a, float &b) {
@@ -644,7 +808,7 @@ __device__ __forceinline__ bool always_bundle_keep(const float4 *always, uint32_
 __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__restrict__ rays, uint32_t ld,
                                               uint32_t off, const uint32_t *__restrict__ alive, uint32_t n,
                                               const Work &w, unsigned long long *counters, uint32_t i, uint32_t *stk,
-                                              float *bl) {
+                                              float *bl, uint32_t *pend) {
   uint32_t c_nodes = 0, c_leaves = 0, c_gates = 0;  // work counters (with counters on; wave-uniform)
   bool active = i < n && (alive == nullptr || alive[off + i] != BZR_RR_NONE);
   f3 s = mk(0.0f, 0.0f, 0.0f), d = s;
@@ -666,6 +830,70 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
   int sp = 0;  // the node to visit next stays in a scalar register; the other hit children go to stk
   uint32_t next = (m.n > 0 && __any(active)) ? 0u : 0xFFFFFFFFu;
   unsigned long long next_hm = 0ull;
+#if BZR_TRAV_BUNDLE
+  // the bundle walk (trace_segment's): batches of up to 16 nodes against the wave's ray bundle, hit leaves
+  // queued in pend and gate-tested by every active lane
+  const bool walk = next != 0xFFFFFFFFu;
+  if (walk) {
+#if BZR_BUNDLE_DPP
+    bundle_setup_dpp(active, s, d, bl, threadIdx.x & 63u);
+#else
+    bundle_to_lds(active, s, d, bl, threadIdx.x & 63u);
+    bundle_derive(bl, threadIdx.x & 63u);
+#endif
+    if ((threadIdx.x & 63u) == 0u) stk[0] = 0u;
+    sp = 1;
+    next = 0xFFFFFFFFu;
+  }
+  const float4 *kids = near_tier ? m.kids_near : m.kids;
+  uint32_t npend = 0, pi = 0;
+  for (;;) {
+    if (pi < npend) {
+      const uint32_t slot = __builtin_amdgcn_readfirstlane(pend[pi]);
+      ++pi;
+      const u32x16 r = *((const cu32x16 *)(uintptr_t)leaf + slot);
+      if (counters) {
+        ++c_leaves;
+        c_gates += (uint32_t)__popcll(__ballot(active));
+      }
+      if (active & planar_gate(leaf_q(r, 0), leaf_q(r, 1), leaf_q(r, 2), leaf_q(r, 3), s, d)) {
+        if (cnt < kMaxCand) w.cand[(size_t)cnt * n + i] = r[15];
+        cnt = cnt < kMaxCand ? cnt + 1 : kOverflow;
+      }
+      continue;
+    }
+    if (sp == 0) break;
+    pi = npend = 0;
+    const uint32_t top = __builtin_amdgcn_readfirstlane(stk[sp - 1]);
+    if (top & bzr_host::kObbFlag) {  // an oriented-box node: its children tested by each lane's own ray
+      --sp;
+      if (counters) ++c_nodes;
+      bool hit[4];
+      uint32_t ch[4];
+      node_children(nodes, obb, top, active, s, d, sinv, inv, hit, ch);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const unsigned long long hm = __ballot(hit[c]);
+        if (hm == 0ull) continue;
+        if (ch[c] & bzr_host::kLeafFlag) {
+          if ((threadIdx.x & 63u) == 0u) pend[npend] = ch[c] & ~bzr_host::kLeafFlag;
+          ++npend;
+        } else if (sp < kStack) {
+          if ((threadIdx.x & 63u) == 0u) stk[sp] = ch[c];
+          ++sp;
+        } else if ((hm >> (threadIdx.x & 63u)) & 1ull) {
+          cnt = kOverflow;  // stack exhausted: full scan
+        }
+      }
+      continue;
+    }
+    bool full;
+    uint32_t k;
+    npend = bundle_batch(kids, stk, sp, pend, bl, threadIdx.x & 63u, full, k);
+    if (full && active) cnt = kOverflow;  // stack exhausted: every active lane takes the full scan
+    if (counters) c_nodes += k;
+  }
+#else
   while (next != 0xFFFFFFFFu || sp > 0) {
     const uint32_t node = next != 0xFFFFFFFFu ? next : __builtin_amdgcn_readfirstlane(stk[--sp]);
     next = 0xFFFFFFFFu;
@@ -701,9 +929,13 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
       }
     }
   }
+#endif
   // the always list (patches without a proven gate region, bvh.cpp): gate-tested for every active ray
   if (m.n_always && __any(active)) {
-    bundle_to_lds(active, s, d, bl, threadIdx.x & 63u);
+#if BZR_TRAV_BUNDLE
+    if (!walk)  // (the bundle walk built it already)
+#endif
+      bundle_to_lds(active, s, d, bl, threadIdx.x & 63u);
     for (uint32_t ab = 0; ab * 64u < m.n_always; ++ab) {
       unsigned long long am = __ballot(always_bundle_keep(m.always, ab * 64u + (threadIdx.x & 63u), m.n_always, bl));
       for (; am; am &= am - 1ull) {
@@ -787,10 +1019,16 @@ __global__ __launch_bounds__(kTravBlock) void k_traverse(MeshView m, const float
                                                          uint32_t off, const uint32_t *__restrict__ alive, uint32_t n,
                                                          Work w, unsigned long long *counters) {
   __shared__ uint32_t stack[kTravBlock / 64][kStack];
-  __shared__ float bundle[kTravBlock / 64][kBundleWords];  // the wave's always-list bundle (always_bundle_keep)
+  __shared__ float bundle[kTravBlock / 64][kBundleWords];  // the wave's ray bundle (bundle walk, always list)
+#if BZR_TRAV_BUNDLE
+  __shared__ uint32_t pend[kTravBlock / 64][64];           // the bundle walk's queued leaf slots
+  uint32_t *wpend = pend[threadIdx.x >> 6];
+#else
+  uint32_t *wpend = nullptr;
+#endif
   const uint32_t b = deal_blocks<BZR_TRAV_XCD>(blockIdx.x, gridDim.x);
   traverse_rays(m, rays, ld, off, alive, n, w, counters, b * kTravBlock + threadIdx.x, stack[threadIdx.x >> 6],
-                bundle[threadIdx.x >> 6]);
+                bundle[threadIdx.x >> 6], wpend);
 }
 
 
@@ -1112,6 +1350,11 @@ struct TraceCtr {  // wave-uniform work counters (kCount)
 #endif
 // BZR_TRACE_PARK_HITS (default 1): park cNone results in the intersect kernel (kModeHits) as well: cfg5
 // fused -7.8 % Newton passes, +3.2 % Mrays/s; cfg3 +1 % (profiles/r03_ab_cfg{5,3}_fused_parkhits.jsonl).
+// BZR_TRACE_BUNDLE (default 0): k_trace walks the tree with the wave-bundle test in batches of up to 16
+// nodes (trace_segment) instead of one node at a time with each lane's slab test.
+#ifndef BZR_TRACE_BUNDLE
+#define BZR_TRACE_BUNDLE 0
+#endif
 #ifndef BZR_TRACE_PARK_HITS
 #define BZR_TRACE_PARK_HITS 1
 #endif
@@ -1133,6 +1376,9 @@ struct TraceLds {  // per wave
   unsigned long long emask[kEntries];        // collected leaves: gate ballot
   float bundle[kBundleWords];                // the always list's ray bundle (always_bundle_keep)
   uint32_t eid[kEntries];                    // and patch index
+#if BZR_TRACE_BUNDLE
+  uint32_t pend[64];                         // the bundle walk's queued leaf slots
+#endif
   float park[TraceWords<kMode>::kPark ? TraceWords<kMode>::kPark : 1][64];
 };
 
@@ -1263,11 +1509,82 @@ __device__ __forceinline__ void trace_segment(const MeshView &m, f3 s, f3 d, boo
   // built once per segment into LDS, so no register holds it across the walk and the Newton passes)
   uint32_t ab = (m.n_always && __any(act)) ? 0u : (m.n_always + 63u) / 64u;  // next batch
   unsigned long long am = 0ull;  // the current batch's patches left to gate-test
+#if BZR_TRACE_BUNDLE
+  // The bundle walk: the wave's active rays as one bundle (bundle_box), the tree taken in batches of up to
+  // 16 nodes -- one child per lane -- from the top of the LDS stack; hit inner children are pushed, hit
+  // leaves queued (L.pend) and gate-tested one by one with every active lane's own exact planar gate.
+  uint32_t npend = 0, pi = 0;  // queued leaves, next to gate-test (uniform)
+  const float4 *kids = near_tier ? m.kids_near : m.kids;
+  if (next != kNo) {
+#if BZR_BUNDLE_DPP
+    bundle_setup_dpp(act, s, d, L.bundle, lane);
+#else
+    bundle_to_lds(act, s, d, L.bundle, lane);
+    bundle_derive(L.bundle, lane);
+#endif
+    if (lane == 0u) L.stack[0] = 0u;
+    sp = 1;
+    next = kNo;
+  }
+#endif
   for (;;) {
     uint32_t ne = 0;  // collected leaves (uniform)
 #if BZR_TRACE_PRIO
     __builtin_amdgcn_s_setprio(BZR_TRACE_PRIO);  // the walk is latency-bound: issue it ahead of Newton passes
 #endif
+#if BZR_TRACE_BUNDLE
+    while (ne < kEntries) {
+      if (pi < npend) {  // a queued leaf: every active lane's planar gate
+        const uint32_t slot = __builtin_amdgcn_readfirstlane(L.pend[pi]);
+        ++pi;
+        const u32x16 r = *((const cu32x16 *)(uintptr_t)leaf + slot);
+        const bool pass = act & planar_gate(leaf_q(r, 0), leaf_q(r, 1), leaf_q(r, 2), leaf_q(r, 3), s, d);
+        if (kCount) {
+          ++ctr.leaves;
+          ctr.gate_tests += popc64(__ballot(act));
+        }
+        const unsigned long long pm = __ballot(pass);
+        if (pm) {
+          if (lane == 0u) {
+            L.eid[ne] = r[15];
+            L.emask[ne] = pm;
+          }
+          ++ne;
+        }
+        continue;
+      }
+      if (sp == 0) break;
+      pi = npend = 0;
+      const uint32_t top = __builtin_amdgcn_readfirstlane(L.stack[sp - 1]);
+      if (top & bzr_host::kObbFlag) {  // an oriented-box node: its children tested by each lane's own ray
+        --sp;
+        if (kCount) ++ctr.nodes;
+        bool hit[4];
+        uint32_t ch[4];
+        node_children(nodes, obb, top, act, s, d, sinv, inv, hit, ch);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const unsigned long long hm = __ballot(hit[c]);
+          if (hm == 0ull) continue;
+          if (ch[c] & bzr_host::kLeafFlag) {
+            if (lane == 0u) L.pend[npend] = ch[c] & ~bzr_host::kLeafFlag;
+            ++npend;
+          } else if (sp < kStack) {
+            if (lane == 0u) L.stack[sp] = ch[c];
+            ++sp;
+          } else if (lane_bit(hm, lane)) {
+            ovf = true;  // traversal stack exhausted: these lanes take the full scan
+          }
+        }
+        continue;
+      }
+      bool full;
+      uint32_t k;
+      npend = bundle_batch(kids, L.stack, sp, L.pend, L.bundle, lane, full, k);
+      if (full) ovf |= act;  // traversal stack exhausted: every active lane takes the full scan
+      if (kCount) ctr.nodes += k;
+    }
+#else
     while ((next != kNo || sp > 0) && ne + 4u <= kEntries) {
       const uint32_t node = next != kNo ? next : __builtin_amdgcn_readfirstlane(L.stack[--sp]);
       next = kNo;
@@ -1285,7 +1602,11 @@ __device__ __forceinline__ void trace_segment(const MeshView &m, f3 s, f3 d, boo
           const float4 g1 = make_float4(__uint_as_float(r[4]), __uint_as_float(r[5]), __uint_as_float(r[6]), __uint_as_float(r[7]));
           const float4 g2 = make_float4(__uint_as_float(r[8]), __uint_as_float(r[9]), __uint_as_float(r[10]), __uint_as_float(r[11]));
           const float4 g3 = make_float4(__uint_as_float(r[12]), __uint_as_float(r[13]), __uint_as_float(r[14]), 0.0f);
-          const bool pass = hit[c] & planar_gate(g0, g1, g2, g3, s, d);
+          const bool pass = hit[c] & planar_gate(g0, g1, g2, g3, s, d)
+#if BZR_DIAG_WALK2
+                            & planar_gate(g0, g1, g2, g3, opaque(s), opaque(d))
+#endif
+              ;
           if (kCount) {
             ++ctr.leaves;
             ctr.gate_tests += popc64(hm);
@@ -1308,12 +1629,13 @@ __device__ __forceinline__ void trace_segment(const MeshView &m, f3 s, f3 d, boo
         }
       }
     }
+#endif
     // tree done: the always list (patches without a proven gate region, bvh.cpp), gate-tested by every
     // wave-segment -- the candidates no box may cull
-    while (next == kNo && sp == 0 && ne < kEntries) {
+    while (next == kNo && sp == 0 && ne < kEntries) {  // (bundle walk: its leaf queue is empty here too)
       if (am == 0ull) {
         if (ab * 64u >= m.n_always) break;
-        if (ab == 0u) bundle_to_lds(act, s, d, L.bundle, lane);
+        if (ab == 0u && !BZR_TRACE_BUNDLE) bundle_to_lds(act, s, d, L.bundle, lane);
         am = __ballot(always_bundle_keep(m.always, ab * 64u + lane, m.n_always, L.bundle));
         ++ab;
         continue;
@@ -1385,7 +1707,16 @@ __device__ __forceinline__ void trace_segment(const MeshView &m, f3 s, f3 d, boo
       }
       uint32_t what = kNone;
       if (run0 || joined || spec) {
+#if BZR_DIAG_NEWTON2
+        // the extra evaluation first, folded to one word, so it adds ~1 live register to the real one
+        const Hit h2 = patch_intersect<false, kFast>(hp, opaque(s), opaque(d), joined || spec);
+        const uint32_t k2 = __float_as_uint(h2.t) ^ h2.what ^ __float_as_uint(h2.normal.x) ^ __float_as_uint(h2.point.y);
+        Hit h = patch_intersect<false, kFast>(hp, s, d, joined || spec);
+        if (k2 != (__float_as_uint(h.t) ^ h.what ^ __float_as_uint(h.normal.x) ^ __float_as_uint(h.point.y)))
+          h.what = kNone;  // never (the same evaluation): keeps h2's whole evaluation
+#else
         const Hit h = patch_intersect<false, kFast>(hp, s, d, joined || spec);
+#endif
         if (spec) {
           park(h, L, lane);
           parked_nb = b;
@@ -1456,8 +1787,13 @@ struct TraceJob {
 #ifndef BZR_TRACE_WPE
 #define BZR_TRACE_WPE 6
 #endif
+// BZR_TRACE_WPE_CHAIN (default BZR_TRACE_WPE): the same bound for the refraction kernels (kModeRefract,
+// kModeStage), which hold 72 VGPRs = 7 waves per SIMD by themselves (7 here trades SGPRs for spills).
+#ifndef BZR_TRACE_WPE_CHAIN
+#define BZR_TRACE_WPE_CHAIN BZR_TRACE_WPE
+#endif
 #if BZR_TRACE_WPE
-#define BZR_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(BZR_TRACE_WPE)))
+#define BZR_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(kMode == kModeHits ? BZR_TRACE_WPE : BZR_TRACE_WPE_CHAIN)))
 #else
 #define BZR_TRACE_ATTR
 #endif
@@ -1653,7 +1989,7 @@ struct DeviceGuard {
 
 MeshView view_of(const bzr_mesh *m, float ri = 1.0f) {
   return MeshView{m->planar, m->full, m->nodes, m->leaf, m->nodes_near, m->leaf_near, m->obb, m->obb_near,
-                  m->always, m->n_always, m->n, m->s_max, m->s_near, ri};
+                  m->always, m->kids, m->kids_near, m->n_always, m->n, m->s_max, m->s_near, ri};
 }
 unsigned grid_for(uint32_t n) { return (n + kBlock - 1) / kBlock; }
 size_t round256(size_t b) { return (b + 255) & ~size_t(255); }
@@ -2101,6 +2437,19 @@ extern "C" bzr_status bzr_mesh_create(bzr_ctx *ctx, const void *patches, uint32_
     return leaf;
   };
   const std::vector<float4> leaf = leaves(bvh), leaf_near = leaves(bvh_near);
+  auto kids_of = [](bzr_host::Bvh const &t) {  // node i, child c -> float4 pair 2 (4 i + c): lo.xyz ref, hi.xyz 0
+    std::vector<float4> k(t.nodes4.size() * 8);
+    for (size_t i = 0; i < t.nodes4.size(); ++i)
+      for (int c = 0; c < 4; ++c) {
+        auto const &nd = t.nodes4[i];
+        float ref;
+        std::memcpy(&ref, &nd.child[c], 4);
+        k[8 * i + 2 * c] = make_float4(nd.lo[0][c], nd.lo[1][c], nd.lo[2][c], ref);
+        k[8 * i + 2 * c + 1] = make_float4(nd.hi[0][c], nd.hi[1][c], nd.hi[2][c], 0.0f);
+      }
+    return k;
+  };
+  const std::vector<float4> kids = kids_of(bvh), kids_near = kids_of(bvh_near);
   // the always list: the same patches in both tiers (whether a gate region is proven does not depend on
   // the tier's origin radius)
   if (bvh.always != bvh_near.always) return set_error(BZR_ERR_INVALID_ARGUMENT, "BVH tiers disagree on the always list");
@@ -2136,6 +2485,8 @@ extern "C" bzr_status bzr_mesh_create(bzr_ctx *ctx, const void *patches, uint32_
       {reinterpret_cast<void **>(&mesh->obb_near), bvh_near.obb.data(),
        bvh_near.obb.size() * sizeof(bzr_host::Bvh4ObbNode)},
       {reinterpret_cast<void **>(&mesh->always), always.data(), always.size() * sizeof(float4)},
+      {reinterpret_cast<void **>(&mesh->kids), kids.data(), kids.size() * sizeof(float4)},
+      {reinterpret_cast<void **>(&mesh->kids_near), kids_near.data(), kids_near.size() * sizeof(float4)},
   };
   hipError_t e = hipSuccess;
   for (auto &u : ups) {
@@ -2165,6 +2516,8 @@ extern "C" bzr_status bzr_mesh_destroy(bzr_mesh *mesh) {
   (void)hipFree(mesh->obb);
   (void)hipFree(mesh->obb_near);
   (void)hipFree(mesh->always);
+  (void)hipFree(mesh->kids);
+  (void)hipFree(mesh->kids_near);
   delete mesh;
   return BZR_OK;
 }

@@ -1002,6 +1002,148 @@ extern "C" int32_t bzr_debug_traverse(const void *patches, uint32_t n, uint32_t 
   return 0;
 }
 
+namespace {
+// Host mirror of the device's wave-bundle box test (trace.hip bundle_box): origins in [sl, sh], directions in
+// [dl, dh] (per axis); see there for the derivation.  rl / rh: 1 / the clamped direction bounds, mixed: the
+// axis's clamped bounds straddle zero.
+struct BundleH {
+  float sl[3], sh[3], rl[3], rh[3];
+  bool mixed[3];
+  bool finite;
+};
+BundleH bundle_h(const float (*s)[3], const float (*d)[3], const bool *act, uint32_t lanes) {
+  BundleH b{};
+  const float inf = HUGE_VALF;
+  float dl[3], dh[3];
+  for (int a = 0; a < 3; ++a) b.sl[a] = dl[a] = inf, b.sh[a] = dh[a] = -inf;
+  for (uint32_t l = 0; l < lanes; ++l)
+    if (act[l])
+      for (int a = 0; a < 3; ++a) {
+        b.sl[a] = std::fmin(b.sl[a], s[l][a]);
+        b.sh[a] = std::fmax(b.sh[a], s[l][a]);
+        dl[a] = std::fmin(dl[a], d[l][a]);
+        dh[a] = std::fmax(dh[a], d[l][a]);
+      }
+  b.finite = true;
+  for (int a = 0; a < 3; ++a) {
+    b.finite &= std::fabs(b.sl[a]) <= 1e30f && std::fabs(b.sh[a]) <= 1e30f && std::fabs(dl[a]) <= 1e30f && std::fabs(dh[a]) <= 1e30f;
+    const float lo = dl[a] > 1e-20f ? dl[a] : std::fmin(dl[a], -1e-20f);
+    const float hi = dh[a] < -1e-20f ? dh[a] : std::fmax(dh[a], 1e-20f);
+    b.rl[a] = 1.0f / lo;
+    b.rh[a] = 1.0f / hi;
+    b.mixed[a] = lo < 0.0f && hi > 0.0f;
+  }
+  return b;
+}
+bool bundle_box_h(const BundleH &b, const float lo[3], const float hi[3]) {
+  if (!b.finite) return true;
+  float tn = -HUGE_VALF, tf = HUGE_VALF;
+  for (int a = 0; a < 3; ++a) {
+    const float A = (hi[a] - b.sl[a]) * b.rl[a], B = (lo[a] - b.sh[a]) * b.rh[a];
+    tn = std::fmax(tn, b.mixed[a] ? std::fmax(A, B) : std::fmin(A, B));
+    tf = std::fmin(tf, b.mixed[a] ? HUGE_VALF : std::fmax(A, B));
+  }
+  tn -= std::fabs(tn) * 0x1p-21f + 0x1p-126f;
+  tf += std::fabs(tf) * 0x1p-21f + 0x1p-126f;
+  return !(tn > tf) && !(tf < 0.0f);  // NaN keeps the box
+}
+}  // namespace
+
+// Host replay of a wave-bundle walk (diagnostic): per 64-ray wave, the tree is walked in batches of up to
+// 16 nodes (64 child slots, one per lane) with the bundle box test instead of each lane's slab test, and
+// compared with the per-lane walk of bzr_debug_traverse.  stats: [0] waves, [1] bundle batches, [2] bundle
+// leaves, [3] per-lane node visits, [4] per-lane leaves, [5] per-lane leaves the bundle missed (must be 0),
+// [6] child slots tested, [7] deepest work stack (nodes).  Oriented-box nodes are walked per lane in both.
+extern "C" int32_t bzr_debug_traverse_bundle(const void *patches, uint32_t n, uint32_t stride, const float *rays,
+                                             uint32_t nr, uint64_t stats[8]) {
+  if ((!patches && n) || (!rays && nr) || !stats || stride % 4 || stride < 264) return 1;
+  bzr_host::Bvh far = bzr_host::build_bvh(static_cast<const float *>(patches), n, stride / 4, bzr_host::kTierFar);
+  bzr_host::Bvh near = bzr_host::build_bvh(static_cast<const float *>(patches), n, stride / 4, bzr_host::kTierNear);
+  for (int k = 0; k < 8; ++k) stats[k] = 0;
+  for (uint32_t w0 = 0; w0 < nr; w0 += 64) {
+    const uint32_t lanes = std::min<uint32_t>(64, nr - w0);
+    float s[64][3], d[64][3], inv[64][3];
+    bool active[64];
+    bool any_act = false;
+    for (uint32_t l = 0; l < lanes; ++l) {
+      for (int k = 0; k < 3; ++k) {
+        s[l][k] = rays[(size_t)k * nr + w0 + l];
+        d[l][k] = rays[(size_t)(3 + k) * nr + w0 + l];
+        inv[l][k] = safe_inv_h(d[l][k]);
+      }
+      const float am = std::fmax(std::fmax(std::fabs(s[l][0]), std::fabs(s[l][1])), std::fabs(s[l][2]));
+      active[l] = am <= far.s_max && std::isfinite(d[l][0]) && (d[l][0] != 0.0f || d[l][1] != 0.0f || d[l][2] != 0.0f);
+      any_act |= active[l];
+    }
+    if (!any_act || !n) continue;
+    bool all_near = true;
+    for (uint32_t l = 0; l < lanes; ++l)
+      all_near &= !active[l] || std::fmax(std::fmax(std::fabs(s[l][0]), std::fabs(s[l][1])), std::fabs(s[l][2])) <= near.s_max;
+    bzr_host::Bvh const &bvh = all_near ? near : far;
+    stats[0] += 1;
+    // per-lane walk: leaves any lane reaches
+    std::vector<uint32_t> lane_leaves, stack{0u};
+    while (!stack.empty()) {
+      const uint32_t node = stack.back();
+      stack.pop_back();
+      stats[3] += 1;
+      const bool is_obb = node & bzr_host::kObbFlag;
+      for (int c = 0; c < 4; ++c) {
+        const uint32_t child = is_obb ? bvh.obb[node & ~bzr_host::kObbFlag].c[c].child : bvh.nodes4[node].child[c];
+        if (child == bzr_host::kEmptyChild) continue;
+        bool any = false;
+        for (uint32_t l = 0; l < lanes && !any; ++l) {
+          if (!active[l]) continue;
+          if (is_obb) any = obb_h(bvh.obb[node & ~bzr_host::kObbFlag].c[c].f, s[l], d[l]);
+          else {
+            auto const &nd = bvh.nodes4[node];
+            const float lo[3] = {nd.lo[0][c], nd.lo[1][c], nd.lo[2][c]}, hi[3] = {nd.hi[0][c], nd.hi[1][c], nd.hi[2][c]};
+            any = slab_h(lo, hi, s[l], inv[l]);
+          }
+        }
+        if (!any) continue;
+        if (child & bzr_host::kLeafFlag) lane_leaves.push_back(child & ~bzr_host::kLeafFlag);
+        else stack.push_back(child);
+      }
+    }
+    stats[4] += lane_leaves.size();
+    // bundle walk in batches of up to 16 nodes
+    const BundleH b = bundle_h(s, d, active, lanes);
+    std::vector<uint32_t> bundle_leaves, work{0u};
+    while (!work.empty()) {
+      const long room = (64 - (long)work.size()) / 3;  // the device's kStack = 64 rule (trace.hip bundle_batch)
+      const size_t take = std::min<size_t>(std::min<size_t>(16, work.size()), (size_t)std::max(room, 1L));
+      std::vector<uint32_t> batch(work.end() - take, work.end());
+      work.resize(work.size() - take);
+      stats[1] += 1;
+      stats[7] = std::max<uint64_t>(stats[7], work.size() + take);
+      for (uint32_t node : batch) {
+        const bool is_obb = node & bzr_host::kObbFlag;
+        for (int c = 0; c < 4; ++c) {
+          const uint32_t child = is_obb ? bvh.obb[node & ~bzr_host::kObbFlag].c[c].child : bvh.nodes4[node].child[c];
+          if (child == bzr_host::kEmptyChild) continue;
+          stats[6] += 1;
+          bool hit = false;
+          if (is_obb) {
+            for (uint32_t l = 0; l < lanes && !hit; ++l) hit = active[l] && obb_h(bvh.obb[node & ~bzr_host::kObbFlag].c[c].f, s[l], d[l]);
+          } else {
+            auto const &nd = bvh.nodes4[node];
+            const float lo[3] = {nd.lo[0][c], nd.lo[1][c], nd.lo[2][c]}, hi[3] = {nd.hi[0][c], nd.hi[1][c], nd.hi[2][c]};
+            hit = bundle_box_h(b, lo, hi);
+          }
+          if (!hit) continue;
+          if (child & bzr_host::kLeafFlag) bundle_leaves.push_back(child & ~bzr_host::kLeafFlag);
+          else work.push_back(child);
+        }
+      }
+    }
+    stats[2] += bundle_leaves.size();
+    std::sort(bundle_leaves.begin(), bundle_leaves.end());
+    for (uint32_t x : lane_leaves) stats[5] += !std::binary_search(bundle_leaves.begin(), bundle_leaves.end(), x);
+  }
+  return 0;
+}
+
 // The always list of one tier (patches without a proven gate region, ascending): count, and the indices
 // when `out` is not null.
 extern "C" int32_t bzr_debug_always_list(const void *patches, uint32_t n, uint32_t stride, int32_t tier, uint32_t *out,

@@ -525,3 +525,59 @@ def test_always_bundle_keeps_every_wave_with_a_gate_pass(bzr, orc):
         if k == 0:
             assert keep.mean() < 0.15, keep.mean()
     assert passes > 50
+
+
+def traverse_bundle(bzr, patches, rays):
+    """bzr_debug_traverse_bundle stats: waves, batches, bundle leaves, lane node visits, lane leaves,
+    lane leaves the bundle walk missed, child slots, deepest work stack."""
+    L = bzr.lib()
+    fn = L.bzr_debug_traverse_bundle
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
+    fn.restype = ctypes.c_int32
+    p = np.ascontiguousarray(patches, np.float32)
+    r = np.ascontiguousarray(rays, np.float32)
+    st = np.zeros(8, np.uint64)
+    assert fn(p.ctypes.data, len(p), 264, r.ctypes.data, r.shape[1], st.ctypes.data) == 0
+    return st
+
+
+def coherent_waves(rng, waves, centre, spread, jitter):
+    """Waves of 64 nearly parallel rays: a random origin and direction per wave, origins spread over a small
+    square, directions jittered; a quarter of the waves get one exactly-zero direction component."""
+    c = np.asarray(centre, np.float64)
+    out = []
+    for _ in range(waves):
+        o0 = c + rng.uniform(-spread, spread, 3) * 3.0
+        d0 = c + rng.uniform(-spread, spread, 3) - o0
+        d0 /= np.linalg.norm(d0)
+        o = o0 + rng.uniform(-1, 1, (64, 3)) * jitter * spread
+        d = d0 + rng.uniform(-1, 1, (64, 3)) * jitter
+        if rng.random() < 0.25:
+            d[:, rng.integers(0, 3)] = 0.0
+        d /= np.linalg.norm(d, axis=1, keepdims=True)
+        out.append(np.concatenate([o.T, d.T]))
+    return np.concatenate(out, axis=1).astype(np.float32)
+
+
+@pytest.mark.parametrize("cfg_name", ["cfg2", "cfg3", "cfg5"])
+def test_bundle_walk_keeps_every_lane_leaf(bzr, cfg_name):
+    """The bundle walk (trace.hip bundle_box, BZR_TRACE_BUNDLE; host mirror bvh.cpp bundle_box_h) reaches
+    every leaf the per-lane slab walk reaches, for every wave: config primaries (8x8 tiles) and coherent
+    random waves of several spreads, including axis-parallel directions -- a wave-level box test that dropped
+    one would lose a candidate patch."""
+    cfg = CONFIGS[cfg_name]
+    patches = build_lens(bzr.TriMesh, cfg.lenses[0]).bezier_patches()
+    if cfg_name == "cfg5":
+        rng0 = np.random.default_rng(5)
+        keep = np.sort(rng0.choice(len(patches), 20000, replace=False))
+        patches = np.ascontiguousarray(patches[keep])
+    rng = np.random.default_rng(11)
+    side = 256 if cfg_name != "cfg3" else 512
+    grid = grid_rays(cfg, side=side)
+    lo, hi = patches[:, 19:49].reshape(-1, 10, 3).min(axis=(0, 1)), patches[:, 19:49].reshape(-1, 10, 3).max(axis=(0, 1))
+    centre, spread = (lo + hi) / 2, float((hi - lo).max()) / 2
+    for rays in (grid, coherent_waves(rng, 150, centre, spread, 1e-3), coherent_waves(rng, 150, centre, spread, 3e-2)):
+        st = traverse_bundle(bzr, patches, rays)
+        assert st[0] > 0 and st[4] > 0
+        assert st[5] == 0, f"bundle walk missed {int(st[5])} leaves"
+        assert st[2] >= st[4]  # a superset of the per-lane walk's leaves (each counted once per wave)
