@@ -144,13 +144,16 @@ constexpr int kTravBlock = BZR_TRAV_BLOCK;
 #ifndef BZR_NODE_ASM
 #define BZR_NODE_ASM 0
 #endif
-// BZR_BUNDLE_DPP (default 1): the bundle walk's ray bundle from DPP reductions (bundle_setup_dpp).
-#ifndef BZR_BUNDLE_DPP
-#define BZR_BUNDLE_DPP 1
+// BZR_BUNDLE_SPREAD (default 0.5): waves whose ray directions spread wider (bundle_setup_dpp) take the
+// per-lane walk instead of the bundle walk.
+#ifndef BZR_BUNDLE_SPREAD
+#define BZR_BUNDLE_SPREAD 0.5f
 #endif
-// BZR_TRAV_BUNDLE (default 0): k_traverse walks with the wave-bundle test in batches (traverse_rays).
+// BZR_TRAV_BUNDLE (default 1): k_traverse walks with the wave-bundle test in batches (traverse_rays):
+// cfg5 8192^2 staged k_traverse 6.61 -> 5.07 ms per frame, cfg3 0.283 -> 0.235, cfg2 0.134 -> 0.143
+// (profiles/r03s2_ab_bundle_walk.jsonl).
 #ifndef BZR_TRAV_BUNDLE
-#define BZR_TRAV_BUNDLE 0
+#define BZR_TRAV_BUNDLE 1
 #endif
 #ifndef BZR_GATE_FLAT
 #define BZR_GATE_FLAT 1
@@ -642,7 +645,7 @@ __device__ __forceinline__ float wave_reduce_dpp(float v) {
 }
 // The whole bundle (words 0..21: bundle_to_lds's 13 and bundle_derive's 9) with the 12 reductions side by
 // side in DPP form, written by lane 0.
-__device__ __forceinline__ void bundle_setup_dpp(bool act, f3 s, f3 d, float *out, uint32_t lane) {
+__device__ __forceinline__ float bundle_setup_dpp(bool act, f3 s, f3 d, float *out, uint32_t lane) {
   const float inf = __builtin_inff();
   const float r[12] = {
       wave_reduce_dpp<false>(act ? s.x : inf),  wave_reduce_dpp<false>(act ? s.y : inf),
@@ -669,6 +672,8 @@ __device__ __forceinline__ void bundle_setup_dpp(bool act, f3 s, f3 d, float *ou
     }
   }
   __builtin_amdgcn_wave_barrier();
+  // the walk choice's width measure (uniform): the widest direction interval (bvh.cpp bundle_spread_h)
+  return fmaxf(fmaxf(r[9] - r[6], r[10] - r[7]), r[11] - r[8]);
 }
 // The bundle walk's per-axis words (13..21, lane 0 after bundle_to_lds): rl = 1 / Dl', rh = 1 / Dh' and
 // mixed = 1 when Dl' < 0 < Dh', where Dl' <= Dl and Dh' >= Dh are the direction bounds moved away from zero
@@ -716,13 +721,13 @@ __device__ __forceinline__ bool bundle_box(const float *B, float4 lo, float4 hi)
 // taking node q's child c from the AoS child records `kids`.  Hit inner children are pushed, hit leaf slots
 // written to `pend` (returns how many).  Returns with `full` set when the stack could not take every hit
 // child (those subtrees are dropped: the caller sends its active lanes to the full scan).
+template <int kCap>
 __device__ __forceinline__ uint32_t bundle_batch(const float4 *kids, uint32_t *stk, int &sp, uint32_t *pend,
                                                  const float *B, uint32_t lane, bool &full, uint32_t &knodes) {
   const uint32_t q = lane >> 2, c = lane & 3u;
-  // at most (kStack - sp) / 3 nodes (at least one), so their <= 4 children each always fit: the stack then
-  // never overflows while the tree is shallower than (kStack - 1) / 3 levels (a wide bundle degrades to
-  // the per-node depth-first order, not to the full scan)
-  const int room = (kStack - sp) / 3;
+  // at most (kCap - sp) / 3 nodes (at least one), so their <= 4 children each fit: the stack overflows only
+  // from a nearly full stack (a wide bundle; the walk choice sends those to the per-lane walk)
+  const int room = (kCap - sp) / 3;
   const uint32_t kmax = (uint32_t)(sp < 16 ? sp : 16) < (uint32_t)(room > 1 ? room : 1) ? (uint32_t)(sp < 16 ? sp : 16)
                                                                                         : (uint32_t)(room > 1 ? room : 1);
   const uint32_t nd = q < kmax ? stk[sp - 1 - (int)q] : 0u;
@@ -738,10 +743,10 @@ __device__ __forceinline__ uint32_t bundle_batch(const float4 *kids, uint32_t *s
   knodes = k;
   sp -= (int)k;
   const int below = (int)lanes_below(im);
-  if (hit && !isleaf && sp + below < kStack) stk[sp + below] = ref;
+  if (hit && !isleaf && sp + below < kCap) stk[sp + below] = ref;
   const int ni = (int)popc64_(im);
-  full = sp + ni > kStack;
-  sp = full ? kStack : sp + ni;
+  full = sp + ni > kCap;
+  sp = full ? kCap : sp + ni;
   if (hit && isleaf) pend[lanes_below(lm)] = ref & ~bzr_host::kLeafFlag;
   return popc64_(lm);
 }
@@ -833,21 +838,19 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
 #if BZR_TRAV_BUNDLE
   // the bundle walk (trace_segment's): batches of up to 16 nodes against the wave's ray bundle, hit leaves
   // queued in pend and gate-tested by every active lane
-  const bool walk = next != 0xFFFFFFFFu;
+  const bool walk = next != 0xFFFFFFFFu;  // (the bundle words are then in bl, for the always list too)
+  bool bwalk = false;                    // the walk choice (trace_segment's)
+  bool narrow = false;                   // else every node is tested per lane (as oriented-box nodes are)
   if (walk) {
-#if BZR_BUNDLE_DPP
-    bundle_setup_dpp(active, s, d, bl, threadIdx.x & 63u);
-#else
-    bundle_to_lds(active, s, d, bl, threadIdx.x & 63u);
-    bundle_derive(bl, threadIdx.x & 63u);
-#endif
+    narrow = bundle_setup_dpp(active, s, d, bl, threadIdx.x & 63u) <= BZR_BUNDLE_SPREAD;
     if ((threadIdx.x & 63u) == 0u) stk[0] = 0u;
     sp = 1;
     next = 0xFFFFFFFFu;
+    bwalk = true;
   }
   const float4 *kids = near_tier ? m.kids_near : m.kids;
   uint32_t npend = 0, pi = 0;
-  for (;;) {
+  while (bwalk) {
     if (pi < npend) {
       const uint32_t slot = __builtin_amdgcn_readfirstlane(pend[pi]);
       ++pi;
@@ -865,12 +868,15 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
     if (sp == 0) break;
     pi = npend = 0;
     const uint32_t top = __builtin_amdgcn_readfirstlane(stk[sp - 1]);
-    if (top & bzr_host::kObbFlag) {  // an oriented-box node: its children tested by each lane's own ray
+    if (!narrow || (top & bzr_host::kObbFlag)) {  // one node, its children tested by each lane's own ray
       --sp;
       if (counters) ++c_nodes;
       bool hit[4];
       uint32_t ch[4];
-      node_children(nodes, obb, top, active, s, d, sinv, inv, hit, ch);
+      // (the reciprocals computed here, not kept from the segment's start: wide waves are rare, and 6
+        // registers live across the Newton passes would cost occupancy)
+        const f3 linv = mk(safe_inv(d.x), safe_inv(d.y), safe_inv(d.z));
+        node_children(nodes, obb, top, active, s, d, mk(s.x * linv.x, s.y * linv.y, s.z * linv.z), linv, hit, ch);
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const unsigned long long hm = __ballot(hit[c]);
@@ -889,12 +895,12 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
     }
     bool full;
     uint32_t k;
-    npend = bundle_batch(kids, stk, sp, pend, bl, threadIdx.x & 63u, full, k);
+    npend = bundle_batch<kStack>(kids, stk, sp, pend, bl, threadIdx.x & 63u, full, k);
     if (full && active) cnt = kOverflow;  // stack exhausted: every active lane takes the full scan
     if (counters) c_nodes += k;
   }
-#else
-  while (next != 0xFFFFFFFFu || sp > 0) {
+#endif
+  while (next != 0xFFFFFFFFu || sp > 0) {  // the per-lane walk
     const uint32_t node = next != 0xFFFFFFFFu ? next : __builtin_amdgcn_readfirstlane(stk[--sp]);
     next = 0xFFFFFFFFu;
     if (counters) ++c_nodes;
@@ -929,7 +935,6 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
       }
     }
   }
-#endif
   // the always list (patches without a proven gate region, bvh.cpp): gate-tested for every active ray
   if (m.n_always && __any(active)) {
 #if BZR_TRAV_BUNDLE
@@ -1351,7 +1356,9 @@ struct TraceCtr {  // wave-uniform work counters (kCount)
 // BZR_TRACE_PARK_HITS (default 1): park cNone results in the intersect kernel (kModeHits) as well: cfg5
 // fused -7.8 % Newton passes, +3.2 % Mrays/s; cfg3 +1 % (profiles/r03_ab_cfg{5,3}_fused_parkhits.jsonl).
 // BZR_TRACE_BUNDLE (default 0): k_trace walks the tree with the wave-bundle test in batches of up to 16
-// nodes (trace_segment) instead of one node at a time with each lane's slab test.
+// nodes (trace_segment) instead of one node at a time with each lane's slab test.  Measured (same bits):
+// cfg5 fused -6.4 %, cfg3 within 1 %, but cfg4 +2.4 % and cfg2 +1 %: the walk code raises the chain
+// kernel to 79 VGPRs (6 waves per SIMD instead of 7), and forcing 7 spills to scratch (+3.8 %).  Off.
 #ifndef BZR_TRACE_BUNDLE
 #define BZR_TRACE_BUNDLE 0
 #endif
@@ -1368,10 +1375,14 @@ struct TraceWords {
   // kModeHits parks the barycentrics too (11 words): 6.4 KB of LDS per wave, which its 6 waves per SIMD
   // (80 VGPRs) leave room for (24 waves x 6.4 KB <= 160 KB)
   static constexpr int kPark = !BZR_TRACE_SPEC ? 0 : (kMode != kModeHits ? 8 : (BZR_TRACE_PARK_HITS ? 11 : 0));
+  // traversal stack entries: the bundle walk's batches push up to 64 children at once, so the refraction
+  // kernels (4.6 KB of LDS per wave at 7 waves per SIMD) take twice BZR_STACK; the intersect kernel's LDS
+  // (6.5 KB per wave at 6 waves per SIMD) has no room left
+  static constexpr int kStackCap = (BZR_TRACE_BUNDLE && kMode != kModeHits) ? 2 * kStack : kStack;
 };
 template <int kMode>
 struct TraceLds {  // per wave
-  uint32_t stack[kStack];
+  uint32_t stack[TraceWords<kMode>::kStackCap];
   float hit[TraceWords<kMode>::kHit][64];    // the lane's current winner (written only when it improves)
   unsigned long long emask[kEntries];        // collected leaves: gate ballot
   float bundle[kBundleWords];                // the always list's ray bundle (always_bundle_keep)
@@ -1484,6 +1495,7 @@ __device__ __forceinline__ void trace_segment(const MeshView &m, f3 s, f3 d, boo
                                               TraceLds<kMode> &L, uint32_t lane, TraceCtr &ctr) {
   constexpr bool kPark = TraceWords<kMode>::kPark > 0;
   constexpr uint32_t kNo = 0xFFFFFFFFu;
+  constexpr int kCap = TraceWords<kMode>::kStackCap;
   best = ~0ull;
   const float amax = fmaxf(fmaxf(fabsf(s.x), fabsf(s.y)), fabsf(s.z));
   bool ovf = false;  // this lane takes the in-order full scan
@@ -1509,22 +1521,26 @@ __device__ __forceinline__ void trace_segment(const MeshView &m, f3 s, f3 d, boo
   // built once per segment into LDS, so no register holds it across the walk and the Newton passes)
   uint32_t ab = (m.n_always && __any(act)) ? 0u : (m.n_always + 63u) / 64u;  // next batch
   unsigned long long am = 0ull;  // the current batch's patches left to gate-test
+  bool bwalk = false;  // this wave-segment takes the bundle walk
 #if BZR_TRACE_BUNDLE
   // The bundle walk: the wave's active rays as one bundle (bundle_box), the tree taken in batches of up to
   // 16 nodes -- one child per lane -- from the top of the LDS stack; hit inner children are pushed, hit
   // leaves queued (L.pend) and gate-tested one by one with every active lane's own exact planar gate.
   uint32_t npend = 0, pi = 0;  // queued leaves, next to gate-test (uniform)
   const float4 *kids = near_tier ? m.kids_near : m.kids;
+  // the walk choice, per wave-segment: a bundle whose directions spread wider than BZR_BUNDLE_SPREAD (rim
+  // waves of refracted rays, incoherent batches) walks per lane instead -- its hull would reach far more
+  // boxes than its rays do
+  bool narrow = false;  // else every node is tested per lane (the oriented-box nodes always are)
   if (next != kNo) {
-#if BZR_BUNDLE_DPP
-    bundle_setup_dpp(act, s, d, L.bundle, lane);
-#else
-    bundle_to_lds(act, s, d, L.bundle, lane);
-    bundle_derive(L.bundle, lane);
+    narrow = bundle_setup_dpp(act, s, d, L.bundle, lane) <= BZR_BUNDLE_SPREAD;
+#if BZR_BUNDLE_ALWAYS_NARROW
+    narrow = true;  // (A/B knob: no per-lane walk for wide bundles)
 #endif
     if (lane == 0u) L.stack[0] = 0u;
     sp = 1;
     next = kNo;
+    bwalk = true;
   }
 #endif
   for (;;) {
@@ -1533,7 +1549,7 @@ __device__ __forceinline__ void trace_segment(const MeshView &m, f3 s, f3 d, boo
     __builtin_amdgcn_s_setprio(BZR_TRACE_PRIO);  // the walk is latency-bound: issue it ahead of Newton passes
 #endif
 #if BZR_TRACE_BUNDLE
-    while (ne < kEntries) {
+    while (bwalk && ne < kEntries) {
       if (pi < npend) {  // a queued leaf: every active lane's planar gate
         const uint32_t slot = __builtin_amdgcn_readfirstlane(L.pend[pi]);
         ++pi;
@@ -1556,12 +1572,15 @@ __device__ __forceinline__ void trace_segment(const MeshView &m, f3 s, f3 d, boo
       if (sp == 0) break;
       pi = npend = 0;
       const uint32_t top = __builtin_amdgcn_readfirstlane(L.stack[sp - 1]);
-      if (top & bzr_host::kObbFlag) {  // an oriented-box node: its children tested by each lane's own ray
+      if (!narrow || (top & bzr_host::kObbFlag)) {  // one node, its children tested by each lane's own ray
         --sp;
         if (kCount) ++ctr.nodes;
         bool hit[4];
         uint32_t ch[4];
-        node_children(nodes, obb, top, act, s, d, sinv, inv, hit, ch);
+        // (the reciprocals computed here, not kept from the segment's start: wide waves are rare, and 6
+        // registers live across the Newton passes would cost occupancy)
+        const f3 linv = mk(safe_inv(d.x), safe_inv(d.y), safe_inv(d.z));
+        node_children(nodes, obb, top, act, s, d, mk(s.x * linv.x, s.y * linv.y, s.z * linv.z), linv, hit, ch);
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
           const unsigned long long hm = __ballot(hit[c]);
@@ -1569,7 +1588,7 @@ __device__ __forceinline__ void trace_segment(const MeshView &m, f3 s, f3 d, boo
           if (ch[c] & bzr_host::kLeafFlag) {
             if (lane == 0u) L.pend[npend] = ch[c] & ~bzr_host::kLeafFlag;
             ++npend;
-          } else if (sp < kStack) {
+          } else if (sp < kCap) {
             if (lane == 0u) L.stack[sp] = ch[c];
             ++sp;
           } else if (lane_bit(hm, lane)) {
@@ -1580,7 +1599,7 @@ __device__ __forceinline__ void trace_segment(const MeshView &m, f3 s, f3 d, boo
       }
       bool full;
       uint32_t k;
-      npend = bundle_batch(kids, L.stack, sp, L.pend, L.bundle, lane, full, k);
+      npend = bundle_batch<kCap>(kids, L.stack, sp, L.pend, L.bundle, lane, full, k);
       if (full) ovf |= act;  // traversal stack exhausted: every active lane takes the full scan
       if (kCount) ctr.nodes += k;
     }
@@ -1621,7 +1640,7 @@ __device__ __forceinline__ void trace_segment(const MeshView &m, f3 s, f3 d, boo
           }
         } else {
           if (next != kNo) {
-            if (sp < kStack) L.stack[sp++] = next;
+            if (sp < kCap) L.stack[sp++] = next;
             else if (lane_bit(next_hm, lane)) ovf = true;  // traversal stack exhausted: these lanes take the full scan
           }
           next = ch[c];

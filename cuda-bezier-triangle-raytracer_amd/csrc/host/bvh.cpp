@@ -1035,6 +1035,19 @@ BundleH bundle_h(const float (*s)[3], const float (*d)[3], const bool *act, uint
   }
   return b;
 }
+// The wave's bundle width measure of the walk choice (trace.hip bundle_spread): the largest direction
+// interval over the three axes.
+float bundle_spread_h(const float (*s)[3], const float (*d)[3], const bool *act, uint32_t lanes) {
+  (void)s;
+  float w = 0.0f;
+  for (int a = 0; a < 3; ++a) {
+    float lo = HUGE_VALF, hi = -HUGE_VALF;
+    for (uint32_t l = 0; l < lanes; ++l)
+      if (act[l]) lo = std::fmin(lo, d[l][a]), hi = std::fmax(hi, d[l][a]);
+    w = std::fmax(w, hi - lo);
+  }
+  return w;
+}
 bool bundle_box_h(const BundleH &b, const float lo[3], const float hi[3]) {
   if (!b.finite) return true;
   float tn = -HUGE_VALF, tf = HUGE_VALF;
@@ -1055,11 +1068,11 @@ bool bundle_box_h(const BundleH &b, const float lo[3], const float hi[3]) {
 // leaves, [3] per-lane node visits, [4] per-lane leaves, [5] per-lane leaves the bundle missed (must be 0),
 // [6] child slots tested, [7] deepest work stack (nodes).  Oriented-box nodes are walked per lane in both.
 extern "C" int32_t bzr_debug_traverse_bundle(const void *patches, uint32_t n, uint32_t stride, const float *rays,
-                                             uint32_t nr, uint64_t stats[8]) {
+                                             uint32_t nr, float max_spread, uint64_t stats[10]) {
   if ((!patches && n) || (!rays && nr) || !stats || stride % 4 || stride < 264) return 1;
   bzr_host::Bvh far = bzr_host::build_bvh(static_cast<const float *>(patches), n, stride / 4, bzr_host::kTierFar);
   bzr_host::Bvh near = bzr_host::build_bvh(static_cast<const float *>(patches), n, stride / 4, bzr_host::kTierNear);
-  for (int k = 0; k < 8; ++k) stats[k] = 0;
+  for (int k = 0; k < 10; ++k) stats[k] = 0;
   for (uint32_t w0 = 0; w0 < nr; w0 += 64) {
     const uint32_t lanes = std::min<uint32_t>(64, nr - w0);
     float s[64][3], d[64][3], inv[64][3];
@@ -1107,8 +1120,14 @@ extern "C" int32_t bzr_debug_traverse_bundle(const void *patches, uint32_t n, ui
       }
     }
     stats[4] += lane_leaves.size();
-    // bundle walk in batches of up to 16 nodes
+    // bundle walk in batches of up to 16 nodes (or, for a bundle wider than max_spread, the per-lane walk)
     const BundleH b = bundle_h(s, d, active, lanes);
+    if (bundle_spread_h(s, d, active, lanes) > max_spread) {
+      stats[8] += 1;
+      stats[1] += 0;
+      stats[2] += lane_leaves.size();
+      continue;
+    }
     std::vector<uint32_t> bundle_leaves, work{0u};
     while (!work.empty()) {
       const long room = (64 - (long)work.size()) / 3;  // the device's kStack = 64 rule (trace.hip bundle_batch)
@@ -1117,6 +1136,7 @@ extern "C" int32_t bzr_debug_traverse_bundle(const void *patches, uint32_t n, ui
       work.resize(work.size() - take);
       stats[1] += 1;
       stats[7] = std::max<uint64_t>(stats[7], work.size() + take);
+      size_t pushed = 0;
       for (uint32_t node : batch) {
         const bool is_obb = node & bzr_host::kObbFlag;
         for (int c = 0; c < 4; ++c) {
@@ -1133,9 +1153,13 @@ extern "C" int32_t bzr_debug_traverse_bundle(const void *patches, uint32_t n, ui
           }
           if (!hit) continue;
           if (child & bzr_host::kLeafFlag) bundle_leaves.push_back(child & ~bzr_host::kLeafFlag);
-          else work.push_back(child);
+          else {
+            work.push_back(child);
+            ++pushed;
+          }
         }
       }
+      if (work.size() > 64) stats[9] += 1;  // the device's stack would overflow here
     }
     stats[2] += bundle_leaves.size();
     std::sort(bundle_leaves.begin(), bundle_leaves.end());

@@ -39,11 +39,13 @@ int32_t bzr_debug_bounding_sphere(const void *patches, uint32_t n, uint32_t stri
 int32_t bzr_debug_traverse(const void *patches, uint32_t n, uint32_t stride, const float *rays, uint32_t nr,
                            uint8_t *hits, uint64_t stats[4]);
 /* Host replay of the wave-bundle walk (trace.hip BZR_TRACE_BUNDLE: batches of up to 16 nodes tested against
- * the wave's ray bundle) beside the per-lane walk, waves of 64 consecutive rays.  stats[0] waves, [1] bundle
- * batches, [2] bundle leaves, [3] per-lane node visits, [4] per-lane leaves, [5] per-lane leaves the bundle
- * walk missed (0: conservative), [6] child slots tested, [7] deepest work stack.  Returns 0 on success. */
+ * the wave's ray bundle) beside the per-lane walk, waves of 64 consecutive rays; waves whose direction spread
+ * exceeds max_spread take the per-lane walk.  stats[0] waves, [1] bundle batches, [2] leaves (bundle or
+ * per-lane walk), [3] per-lane node visits, [4] per-lane leaves, [5] per-lane leaves the bundle walk missed
+ * (0: conservative), [6] child slots tested, [7] deepest work stack, [8] waves on the per-lane walk, [9]
+ * batches after which the work stack exceeded 64.  Returns 0 on success. */
 int32_t bzr_debug_traverse_bundle(const void *patches, uint32_t n, uint32_t stride, const float *rays, uint32_t nr,
-                                  uint64_t stats[8]);
+                                  float max_spread, uint64_t stats[10]);
 /* Device check of the exact normalized() (Eigen a / sqrt(a.a)): `a` is device memory [3][n], `out` device
  * memory [6][n]: rows 0-2 the product's normalized(a), rows 3-5 the same with the compiler's correctly
  * rounded sqrt and one division per component.  Asynchronous on the context's stream.  ctx is a

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--config", default="cfg4")
     ap.add_argument("--waves", type=int, default=400)
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--spread", type=float, default=float("inf"), help="direction spread above which a wave walks per lane")
     a = ap.parse_args()
     import bzr_amd
     from bzr_amd.configs import CONFIGS, build_lens, pixel_coords, rays_for
@@ -50,7 +51,8 @@ def main():
     L = bzr_amd.lib()
     fn = L.bzr_debug_traverse_bundle
     fn.restype = ctypes.c_int32
-    fn.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_float,
+                   ctypes.c_void_p]
     segs = []
     if cfg.op == "chain":
         alive = np.ones(rays.shape[1], bool)
@@ -63,23 +65,24 @@ def main():
                 cur = np.where(alive[None, :], o, cur).astype(np.float32)
     else:
         segs.append(("primary", 0, rays, np.ones(rays.shape[1], bool)))
-    tot = np.zeros(8, np.uint64)
+    tot = np.zeros(10, np.uint64)
     for name, li, r, al in segs:
         r = r.copy()
         r[:, ~al] = np.float32(0.0)  # dead lanes: zero direction -> inactive in the replay
         r = np.ascontiguousarray(r, np.float32)
         p = np.ascontiguousarray(lenses[li], np.float32)
-        st = (ctypes.c_uint64 * 8)()
-        assert fn(p.ctypes.data, len(p), 264, r.ctypes.data, r.shape[1], st) == 0
+        st = (ctypes.c_uint64 * 10)()
+        assert fn(p.ctypes.data, len(p), 264, r.ctypes.data, r.shape[1], a.spread, st) == 0
         s = np.array(st[:], np.uint64)
         tot += s
         w = max(int(s[0]), 1)
         print(f"{a.config} {name:10s} waves {int(s[0]):5d}  bundle batches/wave {s[1]/w:6.2f}  leaves/wave bundle "
               f"{s[2]/w:6.2f} lane {s[4]/w:6.2f}  lane node visits/wave {s[3]/w:6.2f}  slots/wave {s[6]/w:6.1f}  "
-              f"max frontier {int(s[7])}  missed {int(s[5])}")
+              f"max stack {int(s[7])}  missed {int(s[5])}  per-lane waves {int(s[8])}  overflowing batches {int(s[9])}")
     w = max(int(tot[0]), 1)
     print(f"{a.config} all        waves {int(tot[0]):5d}  bundle batches/wave {tot[1]/w:6.2f}  leaves/wave bundle "
-          f"{tot[2]/w:6.2f} lane {tot[4]/w:6.2f}  lane node visits/wave {tot[3]/w:6.2f}  missed {int(tot[5])}")
+          f"{tot[2]/w:6.2f} lane {tot[4]/w:6.2f}  lane node visits/wave {tot[3]/w:6.2f}  missed {int(tot[5])}  "
+          f"per-lane waves {int(tot[8])}  overflowing batches {int(tot[9])}")
 
 
 if __name__ == "__main__":

@@ -532,12 +532,13 @@ def traverse_bundle(bzr, patches, rays):
     lane leaves the bundle walk missed, child slots, deepest work stack."""
     L = bzr.lib()
     fn = L.bzr_debug_traverse_bundle
-    fn.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_float,
+                   ctypes.c_void_p]
     fn.restype = ctypes.c_int32
     p = np.ascontiguousarray(patches, np.float32)
     r = np.ascontiguousarray(rays, np.float32)
-    st = np.zeros(8, np.uint64)
-    assert fn(p.ctypes.data, len(p), 264, r.ctypes.data, r.shape[1], st.ctypes.data) == 0
+    st = np.zeros(10, np.uint64)
+    assert fn(p.ctypes.data, len(p), 264, r.ctypes.data, r.shape[1], np.float32(np.inf), st.ctypes.data) == 0
     return st
 
 
