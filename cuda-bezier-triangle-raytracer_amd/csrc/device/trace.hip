@@ -149,6 +149,11 @@ constexpr int kTravBlock = BZR_TRAV_BLOCK;
 #ifndef BZR_BUNDLE_SPREAD
 #define BZR_BUNDLE_SPREAD 0.5f
 #endif
+// BZR_TRAV_LEAF_PAIRS (default 1): k_traverse's bundle walk fetches its queued leaves two at a time (cfg5 /
+// cfg3 / cfg2 staged k_traverse -2 to -2.5 %, frames -1 %; profiles/r03s2_ab_leaf_pairs.jsonl).
+#ifndef BZR_TRAV_LEAF_PAIRS
+#define BZR_TRAV_LEAF_PAIRS 1
+#endif
 // BZR_TRAV_BUNDLE (default 1): k_traverse walks with the wave-bundle test in batches (traverse_rays):
 // cfg5 8192^2 staged k_traverse 6.61 -> 5.07 ms per frame, cfg3 0.283 -> 0.235, cfg2 0.134 -> 0.143
 // (profiles/r03s2_ab_bundle_walk.jsonl).
@@ -724,6 +729,9 @@ __device__ __forceinline__ bool bundle_box(const float *B, float4 lo, float4 hi)
 template <int kCap>
 __device__ __forceinline__ uint32_t bundle_batch(const float4 *kids, uint32_t *stk, int &sp, uint32_t *pend,
                                                  const float *B, uint32_t lane, bool &full, uint32_t &knodes) {
+  // (the lane index laundered: lane-derived addresses hoisted out of the walk stayed live across the Newton
+  // passes of k_trace and cost it a wave of occupancy)
+  asm volatile("" : "+v"(lane));
   const uint32_t q = lane >> 2, c = lane & 3u;
   // at most (kCap - sp) / 3 nodes (at least one), so their <= 4 children each fit: the stack overflows only
   // from a nearly full stack (a wide bundle; the walk choice sends those to the per-lane walk)
@@ -852,6 +860,29 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
   uint32_t npend = 0, pi = 0;
   while (bwalk) {
     if (pi < npend) {
+#if BZR_TRAV_LEAF_PAIRS
+      // two queued leaves per step: both 64-byte records in flight together (one wait for two round trips)
+      const bool two = pi + 1u < npend;
+      const uint32_t slot0 = __builtin_amdgcn_readfirstlane(pend[pi]);
+      const uint32_t slot1 = __builtin_amdgcn_readfirstlane(pend[two ? pi + 1u : pi]);
+      pi += two ? 2u : 1u;
+      u32x16 r0, r1;
+      asm volatile("s_load_dwordx16 %0, %2, 0x0\n\ts_load_dwordx16 %1, %3, 0x0\n\ts_waitcnt lgkmcnt(0)"
+                   : "=&s"(r0), "=&s"(r1)
+                   : "s"(leaf + 4u * slot0), "s"(leaf + 4u * slot1));
+      if (counters) {
+        c_leaves += two ? 2u : 1u;
+        c_gates += (two ? 2u : 1u) * (uint32_t)__popcll(__ballot(active));
+      }
+      if (active & planar_gate(leaf_q(r0, 0), leaf_q(r0, 1), leaf_q(r0, 2), leaf_q(r0, 3), s, d)) {
+        if (cnt < kMaxCand) w.cand[(size_t)cnt * n + i] = r0[15];
+        cnt = cnt < kMaxCand ? cnt + 1 : kOverflow;
+      }
+      if (two && (active & planar_gate(leaf_q(r1, 0), leaf_q(r1, 1), leaf_q(r1, 2), leaf_q(r1, 3), s, d))) {
+        if (cnt < kMaxCand) w.cand[(size_t)cnt * n + i] = r1[15];
+        cnt = cnt < kMaxCand ? cnt + 1 : kOverflow;
+      }
+#else
       const uint32_t slot = __builtin_amdgcn_readfirstlane(pend[pi]);
       ++pi;
       const u32x16 r = *((const cu32x16 *)(uintptr_t)leaf + slot);
@@ -863,6 +894,7 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
         if (cnt < kMaxCand) w.cand[(size_t)cnt * n + i] = r[15];
         cnt = cnt < kMaxCand ? cnt + 1 : kOverflow;
       }
+#endif
       continue;
     }
     if (sp == 0) break;

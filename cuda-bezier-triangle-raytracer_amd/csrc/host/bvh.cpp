@@ -1062,17 +1062,88 @@ bool bundle_box_h(const BundleH &b, const float lo[3], const float hi[3]) {
 }
 }  // namespace
 
+// Host mirror of the device planar gate (trace.hip planar_gate, BZR_GATE_FLAT; built with -ffp-contract=off
+// like the device code, so the same float operations in the same order): q = the 16-float planar record.
+bool planar_gate_h(const float q[16], const float s[3], const float d[3]) {
+  const float cs = d[0] * q[0] + (d[1] * q[1] + d[2] * q[2]);
+  const float t = (q[3] - (q[0] * s[0] + (q[1] * s[1] + q[2] * s[2]))) / cs;
+  const float ip[3] = {s[0] + d[0] * t, s[1] + d[1] * t, s[2] + d[2] * t};
+  const bool valid = (std::fabs(cs) >= 0.00001f) & (t > 0.0f) & (std::fabs(t) > -q[4]) & (std::fabs(t) > q[5]);
+  const float b0 = q[6] * ip[0] + (q[7] * ip[1] + q[8] * ip[2]);
+  const float b1 = q[9] * ip[0] + (q[10] * ip[1] + q[11] * ip[2]);
+  const float b2 = q[12] * ip[0] + (q[13] * ip[1] + q[14] * ip[2]);
+  return valid & (b0 >= 0.0f) & (b0 <= 1.0f) & (b1 >= 0.0f) & (b1 <= 1.0f) & (b2 >= 0.0f) & (b2 <= 1.0f);
+}
+// The planar record of patch record r (66 words): the device's `planar` / leaf layout.
+void planar_of(const float *r, float q[16]) {
+  const float *m = r + 49;  // col-major M
+  const float v[16] = {r[0], r[1], r[2], r[3], r[58], r[59], m[0], m[3], m[6], m[1], m[4], m[7], m[2], m[5], m[8], 0.0f};
+  std::memcpy(q, v, sizeof v);
+}
+void ivdot_h(const float n[3], const float lo[3], const float hi[3], float &a, float &b) {
+  a = (n[0] >= 0.0f ? n[0] * lo[0] : n[0] * hi[0]) + (n[1] >= 0.0f ? n[1] * lo[1] : n[1] * hi[1]) +
+      (n[2] >= 0.0f ? n[2] * lo[2] : n[2] * hi[2]);
+  b = (n[0] >= 0.0f ? n[0] * hi[0] : n[0] * lo[0]) + (n[1] >= 0.0f ? n[1] * hi[1] : n[1] * lo[1]) +
+      (n[2] >= 0.0f ? n[2] * hi[2] : n[2] * lo[2]);
+}
+float amax_h(float lo, float hi) { return std::fmax(std::fabs(lo), std::fabs(hi)); }
+// Host mirror of the device leaf pre-test (trace.hip bundle_gate_keep): false only when no ray of the
+// bundle (origins [sl, sh], directions [dl, dh]) can pass the leaf's planar gate.  1/x where the device
+// uses v_rcp_f32 (the 6u widening covers both).
+bool bundle_gate_keep_h(const BundleH &b, const float dl[3], const float dh[3], const float q[16]) {
+  if (!b.finite) return true;
+  constexpr float u = 0x1p-24f;
+  const float n[3] = {q[0], q[1], q[2]};
+  float csl, csh, nsl, nsh;
+  ivdot_h(n, dl, dh, csl, csh);
+  ivdot_h(n, b.sl, b.sh, nsl, nsh);
+  const float mc = 8.0f * u * (std::fabs(n[0]) * amax_h(dl[0], dh[0]) + std::fabs(n[1]) * amax_h(dl[1], dh[1]) +
+                               std::fabs(n[2]) * amax_h(dl[2], dh[2]));
+  const float ms = 8.0f * u * (std::fabs(n[0]) * amax_h(b.sl[0], b.sh[0]) + std::fabs(n[1]) * amax_h(b.sl[1], b.sh[1]) +
+                               std::fabs(n[2]) * amax_h(b.sl[2], b.sh[2]) + std::fabs(q[3]));
+  csl -= mc;
+  csh += mc;
+  const float numl = (q[3] - nsh) - ms, numh = (q[3] - nsl) + ms;
+  if (csl > -0.00001f && csh < 0.00001f) return false;
+  if (!(csl > 0.0f || csh < 0.0f)) return true;
+  const float r1 = 1.0f / csl, r2 = 1.0f / csh;
+  const float a1 = numl * r1, a2 = numl * r2, a3 = numh * r1, a4 = numh * r2;
+  float tlo = std::fmin(std::fmin(a1, a2), std::fmin(a3, a4)), thi = std::fmax(std::fmax(a1, a2), std::fmax(a3, a4));
+  tlo -= 6.0f * u * std::fabs(tlo);
+  thi += 6.0f * u * std::fabs(thi);
+  if (!(thi <= 1e30f)) return true;
+  if (thi <= std::fmax(std::fmax(-q[4], q[5]), 0.0f)) return false;  // t > max(0, -hin, hout) for no ray
+  tlo = std::fmax(tlo, 0.0f);
+  float pl[3], ph[3], pm0 = 0.0f, smax = 0.0f;
+  for (int a = 0; a < 3; ++a) {
+    const float x1 = dl[a] * tlo, x2 = dl[a] * thi, x3 = dh[a] * tlo, x4 = dh[a] * thi;
+    pl[a] = b.sl[a] + std::fmin(std::fmin(x1, x2), std::fmin(x3, x4));
+    ph[a] = b.sh[a] + std::fmax(std::fmax(x1, x2), std::fmax(x3, x4));
+    pm0 = std::fmax(pm0, amax_h(pl[a], ph[a]));
+    smax = std::fmax(smax, amax_h(b.sl[a], b.sh[a]));
+  }
+  const float e = 8.0f * u * (smax + pm0);
+  for (int k = 0; k < 3; ++k) {
+    const float mrow[3] = {q[6 + 3 * k], q[7 + 3 * k], q[8 + 3 * k]};
+    float lo, hi;
+    ivdot_h(mrow, pl, ph, lo, hi);
+    const float eb = (std::fabs(mrow[0]) + std::fabs(mrow[1]) + std::fabs(mrow[2])) * (e + 8.0f * u * pm0) + 1e-30f;
+    if (hi + eb < 0.0f || lo - eb > 1.0f) return false;
+  }
+  return true;
+}
+
 // Host replay of a wave-bundle walk (diagnostic): per 64-ray wave, the tree is walked in batches of up to
 // 16 nodes (64 child slots, one per lane) with the bundle box test instead of each lane's slab test, and
 // compared with the per-lane walk of bzr_debug_traverse.  stats: [0] waves, [1] bundle batches, [2] bundle
 // leaves, [3] per-lane node visits, [4] per-lane leaves, [5] per-lane leaves the bundle missed (must be 0),
 // [6] child slots tested, [7] deepest work stack (nodes).  Oriented-box nodes are walked per lane in both.
 extern "C" int32_t bzr_debug_traverse_bundle(const void *patches, uint32_t n, uint32_t stride, const float *rays,
-                                             uint32_t nr, float max_spread, uint64_t stats[10]) {
+                                             uint32_t nr, float max_spread, uint64_t stats[12]) {
   if ((!patches && n) || (!rays && nr) || !stats || stride % 4 || stride < 264) return 1;
   bzr_host::Bvh far = bzr_host::build_bvh(static_cast<const float *>(patches), n, stride / 4, bzr_host::kTierFar);
   bzr_host::Bvh near = bzr_host::build_bvh(static_cast<const float *>(patches), n, stride / 4, bzr_host::kTierNear);
-  for (int k = 0; k < 10; ++k) stats[k] = 0;
+  for (int k = 0; k < 12; ++k) stats[k] = 0;
   for (uint32_t w0 = 0; w0 < nr; w0 += 64) {
     const uint32_t lanes = std::min<uint32_t>(64, nr - w0);
     float s[64][3], d[64][3], inv[64][3];
@@ -1162,6 +1233,27 @@ extern "C" int32_t bzr_debug_traverse_bundle(const void *patches, uint32_t n, ui
       if (work.size() > 64) stats[9] += 1;  // the device's stack would overflow here
     }
     stats[2] += bundle_leaves.size();
+    // the leaf pre-test: which admitted leaves a bundle-level gate keeps; none whose exact gate some lane
+    // passes may be rejected
+    float dl[3], dh[3];
+    for (int a = 0; a < 3; ++a) {
+      dl[a] = HUGE_VALF;
+      dh[a] = -HUGE_VALF;
+      for (uint32_t l = 0; l < lanes; ++l)
+        if (active[l]) dl[a] = std::fmin(dl[a], d[l][a]), dh[a] = std::fmax(dh[a], d[l][a]);
+    }
+    for (uint32_t slot : bundle_leaves) {
+      float q[16];
+      planar_of(static_cast<const float *>(patches) + (size_t)(stride / 4) * bvh.order[slot], q);
+      const bool keep = bundle_gate_keep_h(b, dl, dh, q);
+      stats[10] += keep;
+      if (!keep)
+        for (uint32_t l = 0; l < lanes; ++l)
+          if (active[l] && planar_gate_h(q, s[l], d[l])) {
+            stats[11] += 1;
+            break;
+          }
+    }
     std::sort(bundle_leaves.begin(), bundle_leaves.end());
     for (uint32_t x : lane_leaves) stats[5] += !std::binary_search(bundle_leaves.begin(), bundle_leaves.end(), x);
   }

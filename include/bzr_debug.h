@@ -43,9 +43,10 @@ int32_t bzr_debug_traverse(const void *patches, uint32_t n, uint32_t stride, con
  * exceeds max_spread take the per-lane walk.  stats[0] waves, [1] bundle batches, [2] leaves (bundle or
  * per-lane walk), [3] per-lane node visits, [4] per-lane leaves, [5] per-lane leaves the bundle walk missed
  * (0: conservative), [6] child slots tested, [7] deepest work stack, [8] waves on the per-lane walk, [9]
- * batches after which the work stack exceeded 64.  Returns 0 on success. */
+ * batches after which the work stack exceeded 64, [10] bundle-walk leaves the leaf pre-test keeps, [11] leaves it
+ * rejected although some lane's exact planar gate passes (0: conservative).  Returns 0 on success. */
 int32_t bzr_debug_traverse_bundle(const void *patches, uint32_t n, uint32_t stride, const float *rays, uint32_t nr,
-                                  float max_spread, uint64_t stats[10]);
+                                  float max_spread, uint64_t stats[12]);
 /* Device check of the exact normalized() (Eigen a / sqrt(a.a)): `a` is device memory [3][n], `out` device
  * memory [6][n]: rows 0-2 the product's normalized(a), rows 3-5 the same with the compiler's correctly
  * rounded sqrt and one division per component.  Asynchronous on the context's stream.  ctx is a

@@ -65,24 +65,26 @@ def main():
                 cur = np.where(alive[None, :], o, cur).astype(np.float32)
     else:
         segs.append(("primary", 0, rays, np.ones(rays.shape[1], bool)))
-    tot = np.zeros(10, np.uint64)
+    tot = np.zeros(12, np.uint64)
     for name, li, r, al in segs:
         r = r.copy()
         r[:, ~al] = np.float32(0.0)  # dead lanes: zero direction -> inactive in the replay
         r = np.ascontiguousarray(r, np.float32)
         p = np.ascontiguousarray(lenses[li], np.float32)
-        st = (ctypes.c_uint64 * 10)()
+        st = (ctypes.c_uint64 * 12)()
         assert fn(p.ctypes.data, len(p), 264, r.ctypes.data, r.shape[1], a.spread, st) == 0
         s = np.array(st[:], np.uint64)
         tot += s
         w = max(int(s[0]), 1)
         print(f"{a.config} {name:10s} waves {int(s[0]):5d}  bundle batches/wave {s[1]/w:6.2f}  leaves/wave bundle "
               f"{s[2]/w:6.2f} lane {s[4]/w:6.2f}  lane node visits/wave {s[3]/w:6.2f}  slots/wave {s[6]/w:6.1f}  "
-              f"max stack {int(s[7])}  missed {int(s[5])}  per-lane waves {int(s[8])}  overflowing batches {int(s[9])}")
+              f"max stack {int(s[7])}  missed {int(s[5])}  per-lane waves {int(s[8])}  overflowing batches {int(s[9])}  "
+              f"pre-test keeps {s[10]/w:6.2f}/wave (wrongly rejected {int(s[11])})")
     w = max(int(tot[0]), 1)
     print(f"{a.config} all        waves {int(tot[0]):5d}  bundle batches/wave {tot[1]/w:6.2f}  leaves/wave bundle "
           f"{tot[2]/w:6.2f} lane {tot[4]/w:6.2f}  lane node visits/wave {tot[3]/w:6.2f}  missed {int(tot[5])}  "
-          f"per-lane waves {int(tot[8])}  overflowing batches {int(tot[9])}")
+          f"per-lane waves {int(tot[8])}  overflowing batches {int(tot[9])}  pre-test keeps {tot[10]/w:6.2f}/wave "
+          f"(wrongly rejected {int(tot[11])})")
 
 
 if __name__ == "__main__":

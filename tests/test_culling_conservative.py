@@ -537,7 +537,7 @@ def traverse_bundle(bzr, patches, rays):
     fn.restype = ctypes.c_int32
     p = np.ascontiguousarray(patches, np.float32)
     r = np.ascontiguousarray(rays, np.float32)
-    st = np.zeros(10, np.uint64)
+    st = np.zeros(12, np.uint64)
     assert fn(p.ctypes.data, len(p), 264, r.ctypes.data, r.shape[1], np.float32(np.inf), st.ctypes.data) == 0
     return st
 
@@ -581,4 +581,5 @@ def test_bundle_walk_keeps_every_lane_leaf(bzr, cfg_name):
         st = traverse_bundle(bzr, patches, rays)
         assert st[0] > 0 and st[4] > 0
         assert st[5] == 0, f"bundle walk missed {int(st[5])} leaves"
+        assert st[11] == 0, f"leaf pre-test rejected {int(st[11])} leaves with a passing gate"
         assert st[2] >= st[4]  # a superset of the per-lane walk's leaves (each counted once per wave)
