@@ -149,6 +149,11 @@ constexpr int kTravBlock = BZR_TRAV_BLOCK;
 #ifndef BZR_BUNDLE_SPREAD
 #define BZR_BUNDLE_SPREAD 0.5f
 #endif
+// BZR_TRAV_PRETEST (default 0): k_traverse's bundle walk pre-tests its queued leaves against the bundle
+// (bundle_gate_keep, 64 leaves per pass) before the per-lane gates.
+#ifndef BZR_TRAV_PRETEST
+#define BZR_TRAV_PRETEST 0
+#endif
 // BZR_TRAV_LEAF_PAIRS (default 1): k_traverse's bundle walk fetches its queued leaves two at a time (cfg5 /
 // cfg3 / cfg2 staged k_traverse -2 to -2.5 %, frames -1 %; profiles/r03s2_ab_leaf_pairs.jsonl).
 #ifndef BZR_TRAV_LEAF_PAIRS
@@ -728,7 +733,8 @@ __device__ __forceinline__ bool bundle_box(const float *B, float4 lo, float4 hi)
 // child (those subtrees are dropped: the caller sends its active lanes to the full scan).
 template <int kCap>
 __device__ __forceinline__ uint32_t bundle_batch(const float4 *kids, uint32_t *stk, int &sp, uint32_t *pend,
-                                                 const float *B, uint32_t lane, bool &full, uint32_t &knodes) {
+                                                 const float *B, uint32_t lane, bool &full, uint32_t &knodes,
+                                                 uint32_t base = 0u) {
   // (the lane index laundered: lane-derived addresses hoisted out of the walk stayed live across the Newton
   // passes of k_trace and cost it a wave of occupancy)
   asm volatile("" : "+v"(lane));
@@ -755,7 +761,7 @@ __device__ __forceinline__ uint32_t bundle_batch(const float4 *kids, uint32_t *s
   const int ni = (int)popc64_(im);
   full = sp + ni > kCap;
   sp = full ? kCap : sp + ni;
-  if (hit && isleaf) pend[lanes_below(lm)] = ref & ~bzr_host::kLeafFlag;
+  if (hit && isleaf) pend[base + lanes_below(lm)] = ref & ~bzr_host::kLeafFlag;
   return popc64_(lm);
 }
 // Interval of n.x over x in [lo, hi] (n fixed).
@@ -816,12 +822,66 @@ __device__ __forceinline__ bool always_bundle_keep(const float4 *always, uint32_
   return !(wlo > w1.x + slack) & !(whi < w0.w - slack);
 }
 
+// Wave-level pre-test of a tree leaf's planar gate (the bundle walk's queued leaves, one per lane): false
+// only when no ray of the bundle (LDS words bl: origins [Sl, Sh], directions [Dl, Dh]) can pass the gate of
+// planar record q0..q3 (planar_gate).  The interval steps and margins of always_bundle_keep (cs and num with
+// the lanes' dot-product rounding, the corner quotients of t widened 6u -- v_rcp_f32 --, the plane points P =
+// S + D T widened by e = 8u (|S| + |P|)), then the gate's own tests over the intervals: t > max(0, -hin,
+// hout) for some ray, and each barycentric row b_k = M_k P (M_k . [Pl, Ph]) within [0, 1] widened by
+// |M_k|_1 (e + 8u |P|) (the lanes' fl(M p) rounding is <= 3u |M_k|_1 |p|, the interval sums' own <= 3u).
+// Host mirror: bvh.cpp bundle_gate_keep_h (tests/test_culling_conservative.py).
+__device__ __forceinline__ bool bundle_gate_keep(const float *B, float4 q0, float4 q1, float4 q2, float4 q3) {
+  if (!(B[12] > 0.0f)) return true;
+  constexpr float u = 0x1p-24f;
+  const f3 n = mk(q0.x, q0.y, q0.z);
+  float csl, csh, nsl, nsh;
+  ivdot(n, mk(B[6], B[7], B[8]), mk(B[9], B[10], B[11]), csl, csh);
+  ivdot(n, mk(B[0], B[1], B[2]), mk(B[3], B[4], B[5]), nsl, nsh);
+  const float mc = 8.0f * u * (fabsf(n.x) * absmax(B[6], B[9]) + fabsf(n.y) * absmax(B[7], B[10]) + fabsf(n.z) * absmax(B[8], B[11]));
+  const float ms = 8.0f * u * (fabsf(n.x) * absmax(B[0], B[3]) + fabsf(n.y) * absmax(B[1], B[4]) + fabsf(n.z) * absmax(B[2], B[5]) + fabsf(q0.w));
+  csl -= mc;
+  csh += mc;
+  const float numl = (q0.w - nsh) - ms, numh = (q0.w - nsl) + ms;
+  if (csl > -0.00001f && csh < 0.00001f) return false;  // |cs| < 1e-5 for every ray
+  if (!(csl > 0.0f || csh < 0.0f)) return true;          // cs of either sign: t unbounded
+  const float r1 = __builtin_amdgcn_rcpf(csl), r2 = __builtin_amdgcn_rcpf(csh);
+  const float a1 = numl * r1, a2 = numl * r2, a3 = numh * r1, a4 = numh * r2;
+  float tlo = fminf(fminf(a1, a2), fminf(a3, a4)), thi = fmaxf(fmaxf(a1, a2), fmaxf(a3, a4));
+  tlo -= 6.0f * u * fabsf(tlo);
+  thi += 6.0f * u * fabsf(thi);
+  if (!(thi <= 1e30f)) return true;                                   // huge or NaN: no bound
+  if (thi <= fmaxf(fmaxf(-q1.x, q1.y), 0.0f)) return false;          // t > max(0, -hin, hout) for no ray
+  tlo = fmaxf(tlo, 0.0f);
+  float pl[3], ph[3], pm0 = 0.0f, smax = 0.0f;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    const float dl = B[6 + a], dh = B[9 + a], sl = B[a], sh = B[3 + a];
+    const float x1 = dl * tlo, x2 = dl * thi, x3 = dh * tlo, x4 = dh * thi;
+    pl[a] = sl + fminf(fminf(x1, x2), fminf(x3, x4));
+    ph[a] = sh + fmaxf(fmaxf(x1, x2), fmaxf(x3, x4));
+    pm0 = fmaxf(pm0, absmax(pl[a], ph[a]));
+    smax = fmaxf(smax, absmax(sl, sh));
+  }
+  const float e = 8.0f * u * (smax + pm0), ep = e + 8.0f * u * pm0;
+  const f3 P0 = mk(pl[0], pl[1], pl[2]), P1 = mk(ph[0], ph[1], ph[2]);
+  const f3 row[3] = {mk(q1.z, q1.w, q2.x), mk(q2.y, q2.z, q2.w), mk(q3.x, q3.y, q3.z)};
+  bool keep = true;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    float lo, hi;
+    ivdot(row[k], P0, P1, lo, hi);
+    const float eb = (fabsf(row[k].x) + fabsf(row[k].y) + fabsf(row[k].z)) * ep + 1e-30f;
+    keep &= !(hi + eb < 0.0f) & !(lo - eb > 1.0f);
+  }
+  return keep;
+}
+
 // Candidate search.  `alive` (optional): a ray is traced iff alive[off + i] != BZR_RR_NONE.
 // One wave's 64 rays i (lane l of the wave holds ray i); `stk` is the wave's LDS stack.
 __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__restrict__ rays, uint32_t ld,
                                               uint32_t off, const uint32_t *__restrict__ alive, uint32_t n,
                                               const Work &w, unsigned long long *counters, uint32_t i, uint32_t *stk,
-                                              float *bl, uint32_t *pend) {
+                                              float *bl, uint32_t *pend, uint32_t *raw) {
   uint32_t c_nodes = 0, c_leaves = 0, c_gates = 0;  // work counters (with counters on; wave-uniform)
   bool active = i < n && (alive == nullptr || alive[off + i] != BZR_RR_NONE);
   f3 s = mk(0.0f, 0.0f, 0.0f), d = s;
@@ -857,7 +917,10 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
     bwalk = true;
   }
   const float4 *kids = near_tier ? m.kids_near : m.kids;
-  uint32_t npend = 0, pi = 0;
+  uint32_t npend = 0, pi = 0;  // leaves queued in pend, next to gate-test (uniform)
+#if BZR_TRAV_PRETEST
+  uint32_t nraw = 0;  // leaves queued in raw, not yet pre-tested
+#endif
   while (bwalk) {
     if (pi < npend) {
 #if BZR_TRAV_LEAF_PAIRS
@@ -897,8 +960,34 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
 #endif
       continue;
     }
+#if BZR_TRAV_PRETEST
+    if (sp == 0 || nraw > 64u) {  // the queued leaves' wave-level gate pre-test: the survivors go to pend
+      if (nraw == 0u) break;
+      pi = npend = 0;
+      for (uint32_t j0 = 0; j0 < nraw; j0 += 64u) {
+        const uint32_t j = j0 + (threadIdx.x & 63u);
+        uint32_t slot = 0u;
+        bool keep = false;
+        if (j < nraw) {
+          slot = raw[j];
+          const float4 *lq = leaf + 4u * slot;
+          keep = bundle_gate_keep(bl, lq[0], lq[1], lq[2], lq[3]);
+        }
+        const unsigned long long km = __ballot(keep);
+        if (keep) pend[npend + lanes_below(km)] = slot;
+        npend += (uint32_t)__popcll(km);
+      }
+      nraw = 0u;
+      continue;
+    }
+    uint32_t *qbuf = raw;  // where this step queues its leaves
+    uint32_t &qn = nraw;
+#else
     if (sp == 0) break;
     pi = npend = 0;
+    uint32_t *qbuf = pend;
+    uint32_t &qn = npend;
+#endif
     const uint32_t top = __builtin_amdgcn_readfirstlane(stk[sp - 1]);
     if (!narrow || (top & bzr_host::kObbFlag)) {  // one node, its children tested by each lane's own ray
       --sp;
@@ -914,8 +1003,8 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
         const unsigned long long hm = __ballot(hit[c]);
         if (hm == 0ull) continue;
         if (ch[c] & bzr_host::kLeafFlag) {
-          if ((threadIdx.x & 63u) == 0u) pend[npend] = ch[c] & ~bzr_host::kLeafFlag;
-          ++npend;
+          if ((threadIdx.x & 63u) == 0u) qbuf[qn] = ch[c] & ~bzr_host::kLeafFlag;
+          ++qn;
         } else if (sp < kStack) {
           if ((threadIdx.x & 63u) == 0u) stk[sp] = ch[c];
           ++sp;
@@ -927,7 +1016,7 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
     }
     bool full;
     uint32_t k;
-    npend = bundle_batch<kStack>(kids, stk, sp, pend, bl, threadIdx.x & 63u, full, k);
+    qn += bundle_batch<kStack>(kids, stk, sp, qbuf, bl, threadIdx.x & 63u, full, k, qn);
     if (full && active) cnt = kOverflow;  // stack exhausted: every active lane takes the full scan
     if (counters) c_nodes += k;
   }
@@ -1058,14 +1147,20 @@ __global__ __launch_bounds__(kTravBlock) void k_traverse(MeshView m, const float
   __shared__ uint32_t stack[kTravBlock / 64][kStack];
   __shared__ float bundle[kTravBlock / 64][kBundleWords];  // the wave's ray bundle (bundle walk, always list)
 #if BZR_TRAV_BUNDLE
-  __shared__ uint32_t pend[kTravBlock / 64][64];           // the bundle walk's queued leaf slots
+  __shared__ uint32_t pend[kTravBlock / 64][BZR_TRAV_PRETEST ? 128 : 64];  // the bundle walk's queued leaf slots
   uint32_t *wpend = pend[threadIdx.x >> 6];
 #else
   uint32_t *wpend = nullptr;
 #endif
+#if BZR_TRAV_BUNDLE && BZR_TRAV_PRETEST
+  __shared__ uint32_t raw[kTravBlock / 64][128];  // leaves before the pre-test (up to two batches' worth)
+  uint32_t *wraw = raw[threadIdx.x >> 6];
+#else
+  uint32_t *wraw = nullptr;
+#endif
   const uint32_t b = deal_blocks<BZR_TRAV_XCD>(blockIdx.x, gridDim.x);
   traverse_rays(m, rays, ld, off, alive, n, w, counters, b * kTravBlock + threadIdx.x, stack[threadIdx.x >> 6],
-                bundle[threadIdx.x >> 6], wpend);
+                bundle[threadIdx.x >> 6], wpend, wraw);
 }
 
 
@@ -1388,9 +1483,11 @@ struct TraceCtr {  // wave-uniform work counters (kCount)
 // BZR_TRACE_PARK_HITS (default 1): park cNone results in the intersect kernel (kModeHits) as well: cfg5
 // fused -7.8 % Newton passes, +3.2 % Mrays/s; cfg3 +1 % (profiles/r03_ab_cfg{5,3}_fused_parkhits.jsonl).
 // BZR_TRACE_BUNDLE (default 0): k_trace walks the tree with the wave-bundle test in batches of up to 16
-// nodes (trace_segment) instead of one node at a time with each lane's slab test.  Measured (same bits):
-// cfg5 fused -6.4 %, cfg3 within 1 %, but cfg4 +2.4 % and cfg2 +1 %: the walk code raises the chain
-// kernel to 79 VGPRs (6 waves per SIMD instead of 7), and forcing 7 spills to scratch (+3.8 %).  Off.
+// nodes (trace_segment) instead of one node at a time with each lane's slab test.  Measured (same bits,
+// profiles/r03s2_ab_trace_bundle.jsonl): cfg5 fused -7 % (29 node visits per wave-segment become ~10
+// batches), but cfg4 +5 to +6 %, cfg2 +2.6 to +3.4 %, cfg3 +1.7 % -- a coherent wave in a 6144-patch lens
+// visits only ~13 nodes, and the bundle setup (12 DPP reductions) and batch bookkeeping cost what the
+// fewer slab tests save -- at 7 waves per SIMD (waves_per_eu(7): 72 VGPRs) as at 6.  Off.
 #ifndef BZR_TRACE_BUNDLE
 #define BZR_TRACE_BUNDLE 0
 #endif
