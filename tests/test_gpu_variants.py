@@ -7,6 +7,10 @@ joined retry state must stay valid across the switch.  The default 64-entry stac
 bench configs, so only this build exercises that path: fused == staged == brute force (and == the oracle
 on cfg2), bit for bit, with the device counters reporting overflow rays.
 
+tracebundle: libbzr with k_trace's wave-bundle walk (-DBZR_TRACE_BUNDLE=1, off by default; k_traverse uses
+it by default): the same checks, fused == staged == brute force (== the oracle on cfg2), including the
+incoherent cfg5 rays whose wide bundles take the per-lane node tests.
+
 The variant runs in a child process (BZR_LIBRARY selects the library; one process = one libbzr).
 """
 import json
@@ -85,4 +89,20 @@ def test_tiny_stack_overflow_path_is_exact():
     # the tiny stack really overflowed on both pipelines (the brute-force scan has no stack)
     for k in ("cfg2_fused", "cfg2_staged", "cfg5_fused", "cfg5_staged"):
         assert out[f"{k}_overflow_rays"] > 0, (k, out)
+    assert out["cfg5_hits"] > 10000
+
+
+@pytest.mark.gpu
+def test_trace_bundle_walk_is_exact():
+    lib = PKG / "lib" / "tracebundle" / "libbzr.so"
+    if not lib.exists():
+        pytest.fail(f"{lib} missing: build() makes the `variants` target")
+    env = dict(os.environ, BZR_LIBRARY=str(lib))
+    res = subprocess.run([sys.executable, "-c", WORKER, str(PKG), str(REPO)], env=env, capture_output=True,
+                         text=True, timeout=110)
+    assert res.returncode == 0, res.stderr[-2000:]
+    out = json.loads(res.stdout.strip().splitlines()[-1])
+    for k, v in out.items():
+        if k.endswith("_equal"):
+            assert v, (k, out)
     assert out["cfg5_hits"] > 10000
