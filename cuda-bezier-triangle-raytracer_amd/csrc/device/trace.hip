@@ -71,8 +71,6 @@ struct bzr_mesh {
   bzr_host::Bvh4ObbNode *obb_near;
   float4 *kids;      // the far tree's children AoS (2 float4 per child: lo.xyz ref, hi.xyz 0): the bundle walk's
   float4 *kids_near; // per-lane child records (kids_of), and the near tree's
-  float *wins;       // the far / near trees' nodes in the plane-window layout (wins_of: 48 words per node)
-  float *wins_near;
   float4 *always;   // 8 float4 per always-tested patch (bvh.hpp Bvh::always): planar record with the patch index
                     // in its last word, then the wedge pre-test (always_wedge: w.xyz L H B C 0) and 8 pad words
   uint32_t n_always;
@@ -163,11 +161,6 @@ constexpr int kTravBlock = BZR_TRAV_BLOCK;
 #ifndef BZR_TRAV_LEAF_PAIRS
 #define BZR_TRAV_LEAF_PAIRS 1
 #endif
-// BZR_NODE_WIN (default 0): k_trace's per-lane walk reads nodes in the plane-window layout when the wave's
-// direction signs agree (node_children_win).
-#ifndef BZR_NODE_WIN
-#define BZR_NODE_WIN 0
-#endif
 // BZR_TRAV_BUNDLE (default 1): k_traverse walks with the wave-bundle test in batches (traverse_rays):
 // cfg5 8192^2 staged k_traverse 6.61 -> 5.07 ms per frame, cfg3 0.283 -> 0.235, cfg2 0.134 -> 0.143
 // (profiles/r03s2_ab_bundle_walk.jsonl).
@@ -205,8 +198,6 @@ struct MeshView {
   const float4 *__restrict__ always;  // patches without a proven gate region: gate-tested by every wave-segment
   const float4 *__restrict__ kids;       // AoS child records of nodes / nodes_near (bzr_mesh)
   const float4 *__restrict__ kids_near;
-  const float *__restrict__ wins;        // plane-window nodes (bzr_mesh; node_children_win)
-  const float *__restrict__ wins_near;
   uint32_t n_always;
   uint32_t n;
   float s_max;
@@ -447,35 +438,6 @@ __device__ __forceinline__ void node_children(const bzr_host::Bvh4Node *nodes, c
 #if BZR_DIAG_WALK2
     hit[c] &= slab(lo, hi, s, opaque(sinv), opaque(inv));
 #endif
-  }
-}
-
-// node_children for an axis-aligned node when every active ray of the wave has the same direction sign on
-// each axis (the walk's uniform octant, off = the window per axis: 0 = positive, 4 = negative): the node in
-// the plane-window layout (bzr_mesh wins, 48 words) gives each axis's near and far planes directly -- one
-// 32-byte load per axis -- so a child costs fma x 6 + max3 + min3 instead of slab()'s fma x 6 + min x 3 +
-// max x 3 + max3 + min3.  The same decisions as slab(): the near plane's fma is the smaller of the two
-// (rounding is monotone), which is what slab's min picks.
-typedef uint32_t u32x8w __attribute__((ext_vector_type(8)));
-typedef uint32_t u32x4w __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void node_children_win(const float *wins, uint32_t ref, uint32_t ox, uint32_t oy, uint32_t oz,
-                                                  bool act, f3 sinv, f3 inv, bool (&hit)[4], uint32_t (&ch)[4]) {
-  const float *base = wins + (size_t)48 * ref;
-  u32x8w wx, wy, wz;
-  u32x4w cc;
-  asm volatile(
-      "s_load_dwordx8 %0, %4, 0x0\n\ts_load_dwordx8 %1, %5, 0x0\n\ts_load_dwordx8 %2, %6, 0x0\n\t"
-      "s_load_dwordx4 %3, %7, 0x0\n\ts_waitcnt lgkmcnt(0)"
-      : "=&s"(wx), "=&s"(wy), "=&s"(wz), "=&s"(cc)
-      : "s"(base + ox), "s"(base + 16 + oy), "s"(base + 32 + oz), "s"(base + 12));
-#pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    ch[c] = cc[c];
-    const float ax = __builtin_fmaf(__uint_as_float(wx[c]), inv.x, -sinv.x), bx = __builtin_fmaf(__uint_as_float(wx[4 + c]), inv.x, -sinv.x);
-    const float ay = __builtin_fmaf(__uint_as_float(wy[c]), inv.y, -sinv.y), by = __builtin_fmaf(__uint_as_float(wy[4 + c]), inv.y, -sinv.y);
-    const float az = __builtin_fmaf(__uint_as_float(wz[c]), inv.z, -sinv.z), bz = __builtin_fmaf(__uint_as_float(wz[4 + c]), inv.z, -sinv.z);
-    const float tnear = fmaxf(fmaxf(ax, ay), az), tfar = fminf(fminf(bx, by), bz);
-    hit[c] = act & (ch[c] != bzr_host::kEmptyChild) & (tnear <= tfar) & (tfar >= 0.0f);
   }
 }
 
@@ -1678,15 +1640,6 @@ __device__ __forceinline__ void trace_segment(const MeshView &m, f3 s, f3 d, boo
   const float4 *leaf = near_tier ? m.leaf_near : m.leaf;
   const f3 inv = mk(safe_inv(d.x), safe_inv(d.y), safe_inv(d.z));
   const f3 sinv = mk(s.x * inv.x, s.y * inv.y, s.z * inv.z);
-#if BZR_NODE_WIN
-  // the wave's direction octant when every active lane shares each axis's sign (node_children_win)
-  const unsigned long long amask = __ballot(act);
-  const unsigned long long nx = __ballot(act && signbit(d.x)), ny = __ballot(act && signbit(d.y)),
-                           nz = __ballot(act && signbit(d.z));
-  const bool win_ok = (nx == 0ull || nx == amask) & (ny == 0ull || ny == amask) & (nz == 0ull || nz == amask);
-  const uint32_t wox = nx ? 4u : 0u, woy = ny ? 4u : 0u, woz = nz ? 4u : 0u;
-  const float *wins = near_tier ? m.wins_near : m.wins;
-#endif
   // The node to visit next is held in a scalar register (`next`); only the other hit children go to the
   // LDS stack, so a descent costs no LDS round trip (same visit order as pushing them all).
   int sp = 0;
@@ -1788,11 +1741,7 @@ __device__ __forceinline__ void trace_segment(const MeshView &m, f3 s, f3 d, boo
       if (kCount) ++ctr.nodes;
       bool hit[4];
       uint32_t ch[4];
-#if BZR_NODE_WIN
-      if (win_ok && !(node & bzr_host::kObbFlag)) node_children_win(wins, node, wox, woy, woz, act, sinv, inv, hit, ch);
-      else
-#endif
-        node_children(nodes, obb, node, act, s, d, sinv, inv, hit, ch);
+      node_children(nodes, obb, node, act, s, d, sinv, inv, hit, ch);
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const unsigned long long hm = __ballot(hit[c]);
@@ -2190,7 +2139,7 @@ struct DeviceGuard {
 
 MeshView view_of(const bzr_mesh *m, float ri = 1.0f) {
   return MeshView{m->planar, m->full, m->nodes, m->leaf, m->nodes_near, m->leaf_near, m->obb, m->obb_near,
-                  m->always, m->kids, m->kids_near, m->wins, m->wins_near, m->n_always, m->n, m->s_max, m->s_near, ri};
+                  m->always, m->kids, m->kids_near, m->n_always, m->n, m->s_max, m->s_near, ri};
 }
 unsigned grid_for(uint32_t n) { return (n + kBlock - 1) / kBlock; }
 size_t round256(size_t b) { return (b + 255) & ~size_t(255); }
@@ -2651,24 +2600,6 @@ extern "C" bzr_status bzr_mesh_create(bzr_ctx *ctx, const void *patches, uint32_
     return k;
   };
   const std::vector<float4> kids = kids_of(bvh), kids_near = kids_of(bvh_near);
-  // node i -> 48 words: per axis a, words 16a.. = lo[4] hi[4] lo[4] and (a == 0) the four child refs, so a
-  // 32-byte window at word 16a (positive direction: near = lo, far = hi) or 16a + 4 (negative: near = hi,
-  // far = lo) holds the near and far planes of the four children (node_children_win)
-  auto wins_of = [](bzr_host::Bvh const &t) {
-    std::vector<float> w(t.nodes4.size() * 48, 0.0f);
-    for (size_t i = 0; i < t.nodes4.size(); ++i) {
-      auto const &nd = t.nodes4[i];
-      for (int a = 0; a < 3; ++a)
-        for (int c = 0; c < 4; ++c) {
-          w[48 * i + 16 * a + c] = nd.lo[a][c];
-          w[48 * i + 16 * a + 4 + c] = nd.hi[a][c];
-          w[48 * i + 16 * a + 8 + c] = nd.lo[a][c];
-        }
-      std::memcpy(&w[48 * i + 12], nd.child, 4 * sizeof(uint32_t));
-    }
-    return w;
-  };
-  const std::vector<float> wins = wins_of(bvh), wins_near = wins_of(bvh_near);
   // the always list: the same patches in both tiers (whether a gate region is proven does not depend on
   // the tier's origin radius)
   if (bvh.always != bvh_near.always) return set_error(BZR_ERR_INVALID_ARGUMENT, "BVH tiers disagree on the always list");
@@ -2706,8 +2637,6 @@ extern "C" bzr_status bzr_mesh_create(bzr_ctx *ctx, const void *patches, uint32_
       {reinterpret_cast<void **>(&mesh->always), always.data(), always.size() * sizeof(float4)},
       {reinterpret_cast<void **>(&mesh->kids), kids.data(), kids.size() * sizeof(float4)},
       {reinterpret_cast<void **>(&mesh->kids_near), kids_near.data(), kids_near.size() * sizeof(float4)},
-      {reinterpret_cast<void **>(&mesh->wins), wins.data(), wins.size() * sizeof(float)},
-      {reinterpret_cast<void **>(&mesh->wins_near), wins_near.data(), wins_near.size() * sizeof(float)},
   };
   hipError_t e = hipSuccess;
   for (auto &u : ups) {
@@ -2739,8 +2668,6 @@ extern "C" bzr_status bzr_mesh_destroy(bzr_mesh *mesh) {
   (void)hipFree(mesh->always);
   (void)hipFree(mesh->kids);
   (void)hipFree(mesh->kids_near);
-  (void)hipFree(mesh->wins);
-  (void)hipFree(mesh->wins_near);
   delete mesh;
   return BZR_OK;
 }
