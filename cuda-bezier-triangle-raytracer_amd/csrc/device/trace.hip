@@ -743,9 +743,8 @@ __device__ __forceinline__ uint32_t bundle_batch(const float4 *kids, uint32_t *s
   const uint32_t q = lane >> 2, c = lane & 3u;
   // at most (kCap - sp) / 3 nodes (at least one), so their <= 4 children each fit: the stack overflows only
   // from a nearly full stack (a wide bundle; the walk choice sends those to the per-lane walk)
-  const int room = (kCap - sp) / 3;
-  const uint32_t kmax = (uint32_t)(sp < 16 ? sp : 16) < (uint32_t)(room > 1 ? room : 1) ? (uint32_t)(sp < 16 ? sp : 16)
-                                                                                        : (uint32_t)(room > 1 ? room : 1);
+  const int room = (kCap - sp) / 3, avail = sp < 16 ? sp : 16;
+  const uint32_t kmax = (uint32_t)(avail < room ? avail : (room > 1 ? room : 1));
   const uint32_t nd = q < kmax ? stk[sp - 1 - (int)q] : 0u;
   const unsigned long long ob = __ballot(c == 0u && q < kmax && (nd & bzr_host::kObbFlag));
   const uint32_t k = ob ? (uint32_t)__builtin_ctzll(ob) >> 2 : kmax;
