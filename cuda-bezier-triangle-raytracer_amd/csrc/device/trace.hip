@@ -618,7 +618,7 @@ __device__ __forceinline__ float wave_maxf(float v) {
 }
 // The 12 reductions one after another (a loop that is not unrolled), each stored to the wave's LDS words as
 // soon as it is done, so only one is in registers at a time; word 12 = 1 when every box bound is finite
-// (false also for an empty bundle, whose boxes are +-inf).  Words 13..21: bundle_derive.
+// (false also for an empty bundle, whose boxes are +-inf).  Words 13..21: bundle_setup_dpp.
 constexpr uint32_t kBundleWords = 22;
 __device__ __forceinline__ void bundle_to_lds(bool act, f3 s, f3 d, float *out, uint32_t lane) {
   const float inf = __builtin_inff();
@@ -655,8 +655,10 @@ __device__ __forceinline__ float wave_reduce_dpp(float v) {
 #undef BZR_DPP_STEP
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
 }
-// The whole bundle (words 0..21: bundle_to_lds's 13 and bundle_derive's 9) with the 12 reductions side by
-// side in DPP form, written by lane 0.
+// The whole bundle with the 12 reductions side by side in DPP form, written by lane 0: words 0..12 as
+// bundle_to_lds, and for the bundle walk 13..21 -- per axis rl = 1 / Dl', rh = 1 / Dh' and mixed = 1 when
+// Dl' < 0 < Dh', where Dl' <= Dl and Dh' >= Dh are the direction bounds moved away from zero (|D'| >= 1e-20:
+// a wider direction box, so a superset of the rays).
 __device__ __forceinline__ float bundle_setup_dpp(bool act, f3 s, f3 d, float *out, uint32_t lane) {
   const float inf = __builtin_inff();
   const float r[12] = {
@@ -686,22 +688,6 @@ __device__ __forceinline__ float bundle_setup_dpp(bool act, f3 s, f3 d, float *o
   __builtin_amdgcn_wave_barrier();
   // the walk choice's width measure (uniform): the widest direction interval (bvh.cpp bundle_spread_h)
   return fmaxf(fmaxf(r[9] - r[6], r[10] - r[7]), r[11] - r[8]);
-}
-// The bundle walk's per-axis words (13..21, lane 0 after bundle_to_lds): rl = 1 / Dl', rh = 1 / Dh' and
-// mixed = 1 when Dl' < 0 < Dh', where Dl' <= Dl and Dh' >= Dh are the direction bounds moved away from zero
-// (|D'| >= 1e-20: a wider direction box, so a superset of the rays).
-__device__ __forceinline__ void bundle_derive(float *out, uint32_t lane) {
-  if (lane == 0u) {
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-      const float dl = out[6 + a], dh = out[9 + a];
-      const float lo = dl > 1e-20f ? dl : fminf(dl, -1e-20f), hi = dh < -1e-20f ? dh : fmaxf(dh, 1e-20f);
-      out[13 + a] = 1.0f / lo;
-      out[16 + a] = 1.0f / hi;
-      out[19 + a] = (lo < 0.0f && hi > 0.0f) ? 1.0f : 0.0f;
-    }
-  }
-  __builtin_amdgcn_wave_barrier();
 }
 // Wave-bundle box test (the bundle walk): false only when no ray s + t d, t >= 0, with s in [Sl, Sh] and d in
 // [Dl', Dh'] (per axis, so a superset of the wave's active rays) meets the box.  On axis a the reachable
