@@ -156,10 +156,6 @@ constexpr int kTravBlock = BZR_TRAV_BLOCK;
 #ifndef BZR_TRAV_PRETEST
 #define BZR_TRAV_PRETEST 1
 #endif
-// BZR_TRACE_LEAF_PAIRS (default 0): k_trace's per-lane walk fetches a node's hit leaves two per wait.
-#ifndef BZR_TRACE_LEAF_PAIRS
-#define BZR_TRACE_LEAF_PAIRS 0
-#endif
 // BZR_TRAV_LEAF_PAIRS (default 1): k_traverse's bundle walk fetches its queued leaves two at a time (cfg5 /
 // cfg3 / cfg2 staged k_traverse -2 to -2.5 %, frames -1 %; profiles/r03s2_ab_leaf_pairs.jsonl).
 #ifndef BZR_TRAV_LEAF_PAIRS
@@ -1731,63 +1727,6 @@ __device__ __forceinline__ void trace_segment(const MeshView &m, f3 s, f3 d, boo
       bool hit[4];
       uint32_t ch[4];
       node_children(nodes, obb, node, act, s, d, sinv, inv, hit, ch);
-#if BZR_TRACE_LEAF_PAIRS
-      // the node's hit leaves gate-tested after its inner children are taken, their 64-byte records fetched
-      // two per wait (children picked by selects, not array indexing: no scratch)
-      uint32_t lm = 0;  // bit c: child c is a hit leaf (uniform)
-      unsigned long long hmv[4];
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const unsigned long long hm = __ballot(hit[c]);
-        hmv[c] = hm;
-        if (hm == 0ull) continue;
-        if (ch[c] & bzr_host::kLeafFlag) {
-          lm |= 1u << c;
-        } else {
-          if (next != kNo) {
-            if (sp < kCap) L.stack[sp++] = next;
-            else if (lane_bit(next_hm, lane)) ovf = true;  // traversal stack exhausted: these lanes take the full scan
-          }
-          next = ch[c];
-          next_hm = hm;
-        }
-      }
-      auto pick = [&](uint32_t c) { return c == 0u ? ch[0] : (c == 1u ? ch[1] : (c == 2u ? ch[2] : ch[3])); };
-      auto pickm = [&](uint32_t c) { return c == 0u ? hmv[0] : (c == 1u ? hmv[1] : (c == 2u ? hmv[2] : hmv[3])); };
-      while (lm) {
-        const uint32_t c0 = (uint32_t)__builtin_ctz(lm);
-        lm &= lm - 1u;
-        const bool two = lm != 0u;
-        const uint32_t c1 = two ? (uint32_t)__builtin_ctz(lm) : c0;
-        if (two) lm &= lm - 1u;
-        const unsigned long long m0 = pickm(c0), m1 = pickm(c1);
-        u32x16 r0, r1;
-        asm volatile("s_load_dwordx16 %0, %2, 0x0\n\ts_load_dwordx16 %1, %3, 0x0\n\ts_waitcnt lgkmcnt(0)"
-                     : "=&s"(r0), "=&s"(r1)
-                     : "s"(leaf + 4u * (pick(c0) & ~bzr_host::kLeafFlag)), "s"(leaf + 4u * (pick(c1) & ~bzr_host::kLeafFlag)));
-        const bool pass0 = lane_bit(m0, lane) & planar_gate(leaf_q(r0, 0), leaf_q(r0, 1), leaf_q(r0, 2), leaf_q(r0, 3), s, d);
-        const bool pass1 = two && (lane_bit(m1, lane) & planar_gate(leaf_q(r1, 0), leaf_q(r1, 1), leaf_q(r1, 2), leaf_q(r1, 3), s, d));
-        if (kCount) {
-          ctr.leaves += two ? 2u : 1u;
-          ctr.gate_tests += popc64(m0) + (two ? popc64(m1) : 0u);
-        }
-        const unsigned long long pm0 = __ballot(pass0), pm1 = __ballot(pass1);
-        if (pm0) {
-          if (lane == 0u) {
-            L.eid[ne] = r0[15];
-            L.emask[ne] = pm0;
-          }
-          ++ne;
-        }
-        if (pm1) {
-          if (lane == 0u) {
-            L.eid[ne] = r1[15];
-            L.emask[ne] = pm1;
-          }
-          ++ne;
-        }
-      }
-#else
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const unsigned long long hm = __ballot(hit[c]);
@@ -1824,7 +1763,6 @@ __device__ __forceinline__ void trace_segment(const MeshView &m, f3 s, f3 d, boo
           next_hm = hm;
         }
       }
-#endif
     }
 #endif
     // tree done: the always list (patches without a proven gate region, bvh.cpp), gate-tested by every
