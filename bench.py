@@ -13,9 +13,18 @@ results bit-identical to the reference restatement (tests/test_gpu_parity.py).  
 (torch.distributed over RCCL).  --scaling strong (default): the fixed side x side image is dealt to the
 ranks as 64x64 tiles round-robin (the north-star's 1->8 GPU scaling on a fixed 4096^2 grid); --scaling
 weak: the image grows to side x (side*N).  Each frame's results are gathered to rank 0 over RCCL inside
-the timed region, double-buffered so frame k's gather overlaps frame k+1's tracing: --gather image
-(default) the per-primary status + segment-count word (4 B; the final rays stay in each rank's HBM),
---gather rays the final rays too (28 B per primary), --gather none nothing (tracing alone).
+the timed region, double-buffered so frame k's gather overlaps frame k+1's tracing (bzr_amd/frame.py layouts):
+--gather compact (the default for the chain configs) every final ray on rank 0 in ~17.6 B per primary: a
+status/segment byte per primary plus the final rays of the primaries that refracted (rank 0 regenerates the
+others from their pixels); --gather rays the 6 final-ray floats + the word (28 B per primary); --gather image
+the per-primary status + segment-count word only (4 B; the default for the intersect configs, whose `what`
+row it carries; the final rays / hits stay in each rank's HBM); --gather none nothing (tracing alone).
+
+--gpus N: N ranks, one process per GPU.  Run bare (no WORLD_SIZE in the environment) with N > 1, bench.py
+starts the N rank processes itself (bzr_amd/launch.py: children with RANK / LOCAL_RANK / WORLD_SIZE and a
+127.0.0.1 rendezvous; the parent touches no GPU and exits with the ranks' status).  Under an external
+launcher (torch.distributed.run) WORLD_SIZE must equal N, else bench.py exits with status 2.  The line
+reports the process group's own world size, the RCCL version and each rank's tile count.
 --inflight F (default 3 for the fused pipeline, 2 otherwise): frame k runs on slot k % F (its own context, stream and output buffers), so
 the next frame's waves fill the GPU while a frame's slowest waves finish; every frame is traced in full.
 
@@ -41,17 +50,27 @@ import numpy as np
 # in main()).  set_hw_queues() keeps a caller's value that is large enough (or any value given through
 # BZR_BENCH_HW_QUEUES) and reports the effective one in config.hw_queues.
 HWQ_WANT = 16
+HWQ_MAX = 32  # the GPU pool refuses a GPU_MAX_HW_QUEUES above 32
 
 
 def set_hw_queues(frames_in_flight: int, world: int) -> str:
     """GPU_MAX_HW_QUEUES for this run (before HIP initialises): the slots need distinct queues, and HIP's
-    default of 4 (which the GPU pool exports) let two slots share one in a probe.  Returns the source."""
+    default of 4 (which the GPU pool exports) let two slots share one in a probe.  Capped at HWQ_MAX (a
+    larger --inflight then warns).  Returns the source.  The value is what this process *requested*: under a
+    profiler that preloads HIP (rocprofv3) the runtime has read the variable before this runs."""
     explicit = os.environ.get("BZR_BENCH_HW_QUEUES")
     if explicit:
+        if explicit.isdigit() and int(explicit) > HWQ_MAX:
+            print(f"bench.py: warning: BZR_BENCH_HW_QUEUES={explicit} capped at {HWQ_MAX}", file=sys.stderr, flush=True)
+            explicit = str(HWQ_MAX)
         os.environ["GPU_MAX_HW_QUEUES"] = explicit
         return "BZR_BENCH_HW_QUEUES"
     have = os.environ.get("GPU_MAX_HW_QUEUES", "")
     need = max(HWQ_WANT, frames_in_flight + (1 if world > 1 else 0))
+    if need > HWQ_MAX:
+        print(f"bench.py: warning: {frames_in_flight} frames in flight want {need} hardware queues; capped at "
+              f"{HWQ_MAX}, so some frame slots will share a queue", file=sys.stderr, flush=True)
+        need = HWQ_MAX
     if have.isdigit() and int(have) >= need:
         return "caller"
     os.environ["GPU_MAX_HW_QUEUES"] = str(need)
@@ -84,8 +103,9 @@ def parse():
     p.add_argument("--config", default="cfg4", choices=["cfg2", "cfg3", "cfg4", "cfg5"])
     p.add_argument("--side", type=int, default=0, help="override rays per image side")
     p.add_argument("--scaling", default="strong", choices=["strong", "weak"])
-    p.add_argument("--gather", default="image", choices=["image", "rays", "compact", "none"],
-                   help="what each frame sends to rank 0 when N > 1 (frame.py layouts, DESIGN.md (e) byte budget)")
+    p.add_argument("--gather", default="auto", choices=["auto", "image", "rays", "compact", "none"],
+                   help="what each frame sends to rank 0 when N > 1 (frame.py layouts, DESIGN.md (e) byte budget); "
+                        "auto = compact for the chain configs (every final ray on rank 0), image for intersect")
     p.add_argument("--accel", default="bvh", choices=["bvh", "none"], help="none = brute-force scan (A/B)")
     p.add_argument("--pipeline", default="fused", choices=["fused", "staged", "auto"],
                    help="culled-path pipeline (include/bzr.h BZR_PIPELINE_*; same output bits): fused = one k_trace "
@@ -210,6 +230,10 @@ def pmc_traffic(kernel, workload):
 
 def main():
     a = parse()
+    from bzr_amd import launch  # no torch, no HIP: safe in the launching parent
+
+    if launch.check_world(a.gpus) == "spawn":  # bare `bench.py --gpus N`: start the N rank processes here
+        raise SystemExit(launch.spawn([sys.executable, str(Path(__file__).resolve())] + sys.argv[1:], a.gpus))
     if a.inflight <= 0:  # the staged pipeline's small kernels contend beyond two frames
         a.inflight = 3 if (a.accel == "bvh" and a.pipeline == "fused") else 2
     hwq_source = set_hw_queues(a.inflight, int(os.environ.get("WORLD_SIZE", "1")))
@@ -233,6 +257,8 @@ def main():
 
     cfg = CONFIGS[a.config]
     chain = cfg.op == "chain"
+    if a.gather == "auto":  # every final ray on rank 0 for the chain; the hit's `what` image for intersect
+        a.gather = "compact" if chain else "image"
     side = a.side or cfg.side
     height = side * world if a.scaling == "weak" else side
     t0 = time.perf_counter()
@@ -264,6 +290,22 @@ def main():
 
     _, _, rays_np = frame.rank_rays(cfg, rank, world, side, height)
     n = rays_np.shape[1]
+    # what actually runs: the process group's own size and every rank's share, as each rank counted it
+    pg_world = dist.get_world_size() if world > 1 else 1
+    if pg_world != a.gpus:
+        raise SystemExit(f"bench.py: process group has {pg_world} ranks, --gpus {a.gpus}")
+    shares = torch.tensor([n // (frame.TILE * frame.TILE)], dtype=torch.int64,
+                          device=dev if (world > 1 and dist.get_backend() == "nccl") else "cpu")
+    if world > 1:
+        parts = [torch.zeros_like(shares) for _ in range(world)]
+        dist.all_gather(parts, shares)
+        tiles_per_rank = [int(p.item()) for p in parts]
+    else:
+        tiles_per_rank = [int(shares.item())]
+    rccl = None
+    if world > 1 and dist.get_backend() == "nccl":
+        v = torch.cuda.nccl.version()
+        rccl = ".".join(str(x) for x in v) if isinstance(v, tuple) else str(v)
     rays = torch.from_numpy(rays_np).to(dev)
     # Frames in flight: frame k runs on slot k % F -- its own context, stream and output buffers -- so the
     # next frame's waves fill the GPU while this frame's slowest waves finish (a frame's last waves run
@@ -465,7 +507,7 @@ def main():
             "metric": "Mrays/sec (primary+refracted) at 1/2/4/8 MI355X; % of HBM-read roofline",
             "value": round(value, 3),
             "unit": "Mrays/s",
-            "n_gpus": world,
+            "n_gpus": pg_world,
             "steps": a.steps,
             "warmup": a.warmup,
             "prewarm_s": a.prewarm_s,
@@ -479,6 +521,10 @@ def main():
                 "workload": f"{cfg.name}: {cfg.note}" + (f" (side {side})" if side != cfg.side else ""),
                 "image": f"{side}x{height}",
                 "primaries_per_gpu": n,
+                "ranks": {"world_size": pg_world, "backend": dist.get_backend() if world > 1 else None,
+                          "rccl_version": rccl, "launcher": os.environ.get(launch.LAUNCHED_BY) or
+                          ("external (WORLD_SIZE set)" if world > 1 else "single process"),
+                          "tiles_per_rank": tiles_per_rank, "tile": f"{frame.TILE}x{frame.TILE}"},
                 "segments_per_step": seg_total,
                 "patches": n_patch,
                 "parallelism": f"64x64 image tiles round-robin over {world} rank(s), {a.scaling} scaling"
@@ -489,7 +535,7 @@ def main():
                            if gather else None),
                 "pipeline": a.pipeline,
                 "frames_in_flight": F,
-                "hw_queues": {"GPU_MAX_HW_QUEUES": hwq, "source": hwq_source,
+                "hw_queues": {"GPU_MAX_HW_QUEUES_requested": hwq, "source": hwq_source,
                               "streams": len(streams) + (1 if gather else 0),
                               "ok": hwq >= len(streams) + (1 if gather else 0)},
                 "scan": "BVH-culled (bit-identical to brute force)" if a.accel == "bvh" else "brute force",

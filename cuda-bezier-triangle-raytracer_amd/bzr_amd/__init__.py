@@ -75,6 +75,14 @@ _SIGS = {
     "bzr_refract": [_P, _P, _F, _P, _P, _U32, _U32, _P, _P, _U32],
     "bzr_trace_chain": [_P, _P, _P, _U32, _P, _U32, _P, _P, _P, _U32],
     "bzr_trace_tiled": [_P, _U32, _P, _P, _U32, _P, _U32, _U32, _P, _P, _P, _U32],
+    "bzr_tiled_create": [_P, _U32, _U32, _U32, _U32, _I32, ctypes.POINTER(_P)],
+    "bzr_tiled_destroy": [_P],
+    "bzr_tiled_info": [_P, _P, _P, _P],
+    "bzr_tiled_set_rays": [_P, _P, _U32],
+    "bzr_tiled_share_rays": [_P, _U32, ctypes.POINTER(_P)],
+    "bzr_tiled_trace": [_P, _P, _P, _U32, _P, _P, _P, _U32],
+    "bzr_tiled_stream": [_P, ctypes.POINTER(_P)],
+    "bzr_tiled_sync": [_P],
     "bzr_mesh_interpolate": [_P, _P, _I32, _P, _U32],
     "bzr_emit": [_P, _P, ctypes.c_uint64, _U32, _P, _P, _U32],
     "bzr_illuminate": [_P, _P, _P, _U32, _P, ctypes.c_uint64, _P, _P, _P, _U32],
@@ -388,23 +396,97 @@ def pack_frame(ctx: Context, layout: str, rays, status, segments, packed, npad: 
     return packed
 
 
-def trace_tiled(ctxs, lenses, ri, rays, tile_rays=4096, mode=MODE_PARITY):
-    """bzr_trace_tiled: the chain over several contexts (one per device) from one process.
-    `lenses[d]` is the list of DeviceMesh living on ctxs[d]; rays are host arrays [6, n], ordered
-    tile-major.  -> (rays [6, n], status [n], segments [n]) in input order."""
+def trace_tiled(ctxs, lenses, ri, rays, tile_rays=4096, mode=MODE_PARITY, out=None):
+    """bzr_trace_tiled: the chain over several contexts (one per device) from one process, gathered to
+    ctxs[0]'s device on the device side.  `lenses[d]` is the list of DeviceMesh living on ctxs[d]; rays
+    [6, n] ordered tile-major, a host array or a tensor on ctxs[0]'s device (then the outputs are tensors
+    there).  -> (rays [6, n], status [n], segments [n]) in input order."""
     nc, nl = len(ctxs), len(ri)
     if len(lenses) != nc or any(len(ls) != nl for ls in lenses):
         raise ValueError("lenses must hold one list of len(ri) meshes per context")
-    r = np.ascontiguousarray(rays, dtype=np.float32)
-    n = r.shape[1]
-    out_rays, out_status, out_segments = np.empty((6, n), np.float32), np.empty(n, np.uint32), np.empty(n, np.uint32)
+    r = _Buf(rays, np.float32)
+    n = _n_of(rays)
+    if out is None:
+        out = (_empty_like(rays, 6, np.float32), _empty_like(rays, 0, np.uint32), _empty_like(rays, 0, np.uint32))
+    o, s_, g = _Buf(out[0], np.float32, True), _Buf(out[1], np.uint32, True), _Buf(out[2], np.uint32, True)
+    res = _residency(r, o, s_, g)
     cs = (_P * nc)(*[c.handle for c in ctxs])
     hs = (_P * (nc * nl))(*[m.handle for ls in lenses for m in ls])
     ris = (_F * nl)(*[float(x) for x in ri])
+    if res == DEVICE_PTRS:
+        import torch
+
+        torch.cuda.current_stream(ctxs[0].device).synchronize()  # torch-made inputs are complete
     _check(lib().bzr_trace_tiled(ctypes.cast(cs, _P), nc, ctypes.cast(hs, _P), ctypes.cast(ris, _P), nl,
-                                 r.ctypes.data, n, tile_rays, out_rays.ctypes.data, out_status.ctypes.data,
-                                 out_segments.ctypes.data, mode))
-    return out_rays, out_status, out_segments
+                                 r.ptr, n, tile_rays, o.ptr, s_.ptr, g.ptr, mode | res))
+    return out
+
+
+GATHER_AUTO, GATHER_RCCL, GATHER_PEER = 0, 1, 2  # BZR_GATHER_*
+
+
+class TiledPlan:
+    """bzr_tiled: multi-device frames from one process, gathered to device 0 on the device side (RCCL over
+    xGMI between distinct devices, peer copies otherwise).  ctxs: nslot lists of ndev contexts (slot s, device
+    d); the frame is n tile-major rays."""
+
+    def __init__(self, ctxs, n: int, tile_rays: int = 4096, transport: int = GATHER_AUTO):
+        slots = [list(s) for s in ctxs]
+        self.ndev, self.nslot = len(slots[0]), len(slots)
+        if any(len(s) != self.ndev for s in slots):
+            raise ValueError("every slot lists the same number of devices")
+        self.ctxs = slots
+        flat = (_P * (self.ndev * self.nslot))(*[c.handle for s in slots for c in s])
+        h = _P()
+        _check(lib().bzr_tiled_create(ctypes.cast(flat, _P), self.ndev, self.nslot, n, tile_rays, transport,
+                                      ctypes.byref(h)))
+        self.handle, self.n, self.tile_rays = h, n, tile_rays
+
+    def info(self):
+        """(transport, rays per device share, npad)"""
+        t, npad = _I32(0), _U32(0)
+        share = np.zeros(self.ndev, np.uint32)
+        _check(lib().bzr_tiled_info(self.handle, ctypes.byref(t), share.ctypes.data, ctypes.byref(npad)))
+        return int(t.value), share, int(npad.value)
+
+    def set_rays(self, rays):
+        r = _Buf(rays, np.float32)
+        if r.device:
+            import torch
+
+            torch.cuda.current_stream(self.ctxs[0][0].device).synchronize()
+        _check(lib().bzr_tiled_set_rays(self.handle, r.ptr, DEVICE_PTRS if r.device else HOST_PTRS))
+
+    def trace(self, lenses, ri, out_rays, out_status, out_segments=None, mode=MODE_PARITY):
+        """One frame; lenses[d] = device d's DeviceMesh list.  Device tensors (on device 0): queued, ready on
+        stream() / after sync(); host arrays: synchronous."""
+        nl = len(ri)
+        hs = (_P * (self.ndev * nl))(*[m.handle for ls in lenses for m in ls])
+        ris = (_F * nl)(*[float(x) for x in ri])
+        o, s_ = _Buf(out_rays, np.float32, True), _Buf(out_status, np.uint32, True)
+        g = _Buf(out_segments, np.uint32, True)
+        res = _residency(o, s_, *([g] if out_segments is not None else []))
+        _check(lib().bzr_tiled_trace(self.handle, ctypes.cast(hs, _P), ctypes.cast(ris, _P), nl, o.ptr, s_.ptr, g.ptr,
+                                     res | mode))
+
+    def stream(self) -> int:
+        p = _P()
+        _check(lib().bzr_tiled_stream(self.handle, ctypes.byref(p)))
+        return int(p.value or 0)
+
+    def sync(self):
+        _check(lib().bzr_tiled_sync(self.handle))
+
+    def close(self):
+        if getattr(self, "handle", None):
+            lib().bzr_tiled_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def interpolate(ctx: Context, mesh: DeviceMesh, divisor: int, out=None):

@@ -1,6 +1,7 @@
-// bridge.cpp -- the drop-in classes' hot-path methods, forwarded to the GPU
-// through the C ABI.  No CPU implementation of intersect/refract exists in the
-// product: without a HIP device these calls throw (bzr::check).
+// bridge.cpp -- the drop-in classes' hot-path methods.  The batch overloads, bzr::traceChain and the
+// multi-device calls forward to the GPU through the C ABI (without a HIP device they throw, bzr::check);
+// the reference's single-ray methods run the same arithmetic on the host (single_ray.cpp, SURVEY.md
+// 8b.1), bit-identical to the batch path, without a launch or PCIe round trip per ray.
 //   BezierTriangle::intersect  reference/bezierTriangle.cpp:123-195
 //   BezierMesh::intersect      reference/bezierMesh.cpp:206-227
 //   BezierLens::refract        reference/bezierLens.cpp:4-34
@@ -11,6 +12,7 @@
 #include <mutex>
 
 #include "bzr/bzr.hpp"
+#include "single_ray.hpp"
 
 namespace bzr {
 
@@ -126,6 +128,59 @@ void traceChainTiled(std::vector<Context *> const &ctxs, std::vector<BezierLens 
   }
 }
 
+TiledChain::TiledChain(std::vector<std::vector<Context *>> const &slots, std::vector<BezierLens const *> const &lenses,
+                       std::size_t n, uint32_t tileRays, int transport) {
+  if (slots.empty() || slots[0].empty()) throw std::invalid_argument("TiledChain: no contexts");
+  if (n == 0 || n > UINT32_MAX) throw std::length_error("TiledChain: frame of 1..2^32-1 rays");
+  mDevices = slots[0].size();
+  mN = n;
+  std::vector<bzr_ctx *> handles;
+  for (auto const &slot : slots) {
+    if (slot.size() != mDevices) throw std::invalid_argument("TiledChain: every slot lists the same devices");
+    for (Context *c : slot) handles.push_back(c->get());
+  }
+  for (auto const *l : lenses) mRi.push_back(l->getRefractiveIndex());
+  for (Context *c : slots[0])  // device d's lens copies (meshes are device-scoped: every slot's context on d uses them)
+    for (auto const *l : lenses) mMeshes.push_back(l->getMesh().device(*c));
+  check(bzr_tiled_create(handles.data(), static_cast<uint32_t>(mDevices), static_cast<uint32_t>(slots.size()),
+                         static_cast<uint32_t>(n), tileRays, transport, &mPlan));
+}
+
+TiledChain::~TiledChain() { bzr_tiled_destroy(mPlan); }
+
+int TiledChain::transport() const {
+  int32_t t = 0;
+  check(bzr_tiled_info(mPlan, &t, nullptr, nullptr));
+  return t;
+}
+
+void TiledChain::setRays(Ray const *rays) {
+  std::vector<float> soa = raysToSoa(rays, mN);
+  check(bzr_tiled_set_rays(mPlan, soa.data(), BZR_HOST_PTRS));
+}
+
+void TiledChain::setRaysDevice(float const *raysSoaOnDevice0) {
+  check(bzr_tiled_set_rays(mPlan, raysSoaOnDevice0, BZR_DEVICE_PTRS));
+}
+
+void TiledChain::trace(float *outRays, uint32_t *outStatus, uint32_t *outSegments, uint32_t flags) {
+  check(bzr_tiled_trace(mPlan, mMeshes.data(), mRi.data(), static_cast<uint32_t>(mRi.size()), outRays, outStatus,
+                        outSegments, flags | BZR_DEVICE_PTRS));
+}
+
+void TiledChain::trace(Ray *outRays, RefractionResult *outStatus, uint32_t *outSegments, uint32_t flags) {
+  std::vector<float> out(6 * mN);
+  std::vector<uint32_t> st(mN);
+  check(bzr_tiled_trace(mPlan, mMeshes.data(), mRi.data(), static_cast<uint32_t>(mRi.size()), out.data(), st.data(),
+                        outSegments, flags & ~uint32_t(BZR_DEVICE_PTRS)));
+  for (std::size_t i = 0; i < mN; ++i) {
+    outRays[i] = soaToRay(out, mN, i);
+    outStatus[i] = static_cast<RefractionResult>(st[i]);
+  }
+}
+
+void TiledChain::sync() { check(bzr_tiled_sync(mPlan)); }
+
 }  // namespace bzr
 
 bzr_mesh *BezierMesh::device(bzr::Context &ctx) const {
@@ -156,21 +211,15 @@ void BezierMesh::intersect(Ray const *rays, std::size_t n, BezierIntersection *o
 }
 
 BezierIntersection BezierMesh::intersect(Ray const &ray) const {
-  BezierIntersection r;
-  intersect(&ray, 1, &r);
-  return r;
+  return bzr::host::meshIntersect(mMesh.data(), mMesh.size(), ray, nullptr);
+}
+
+BezierIntersection BezierMesh::intersect(Ray const &ray, uint32_t *patchIndex) const {
+  return bzr::host::meshIntersect(mMesh.data(), mMesh.size(), ray, patchIndex);
 }
 
 BezierIntersection BezierTriangle::intersect(Ray const &ray, LimitPlaneIntersection limit) const {
-  bzr::Context &c = bzr::defaultContext();
-  bzr_mesh *m = nullptr;
-  bzr::check(bzr_mesh_create(c.get(), this, 1, sizeof(BezierTriangle), &m));
-  std::vector<float> in = bzr::raysToSoa(&ray, 1), hits(13);
-  uint32_t idx = 0, lim = static_cast<uint32_t>(limit);
-  bzr_status s = bzr_patch_intersect(c.get(), m, &idx, &lim, in.data(), 1, hits.data(), BZR_HOST_PTRS);
-  bzr_mesh_destroy(m);
-  bzr::check(s);
-  return bzr::hitFromSoa(hits, 1, 0);
+  return bzr::host::patchIntersect(*this, ray, limit == LimitPlaneIntersection::cNone);
 }
 
 void BezierLens::refract(Ray const *rays, RefractionResult const *expected, std::size_t n, Ray *outRays,
@@ -192,8 +241,5 @@ void BezierLens::refract(Ray const *rays, RefractionResult const *expected, std:
 }
 
 std::pair<Ray, RefractionResult> BezierLens::refract(Ray const &ray, RefractionResult expected) const {
-  Ray out;
-  RefractionResult st;
-  refract(&ray, &expected, 1, &out, &st);
-  return {out, st};
+  return bzr::host::lensRefract(&mMesh[0], mMesh.size(), mRefractiveIndex, ray, expected);
 }

@@ -197,15 +197,55 @@ bzr_status bzr_trace_chain(bzr_ctx *ctx, const bzr_mesh *const *lenses, const fl
                            uint32_t *out_status, uint32_t *out_segments, uint32_t flags);
 /* Multi-GPU refraction chain in ONE process (C/C++ hosts without torch.distributed):
  * image-plane tiles are dealt round-robin to the contexts, one per device.  Tile k is the rays
- * [k * tile_rays, (k + 1) * tile_rays) of the host SoA input (callers order rays tile-major, e.g.
- * 64x64-pixel tiles of 4096 rays); context d traces tiles d, d + nctx, ... through its own copy of
- * the lenses, lenses[d * nlens + l] living on ctxs[d]'s device, on its own host thread, and the
- * results land in the host outputs in input order (same bits as one bzr_trace_chain over all rays).
- * Host pointers only (BZR_DEVICE_PTRS is rejected); synchronous; the mode flags pass through. */
+ * [k * tile_rays, (k + 1) * tile_rays) of the SoA input (callers order rays tile-major, e.g. 64x64-pixel
+ * tiles of 4096 rays); context d traces tiles d, d + nctx, ... through its own copy of the lenses,
+ * lenses[d * nlens + l] living on ctxs[d]'s device, and the results are gathered to ctxs[0]'s device on
+ * the device side (RCCL when the contexts' devices are distinct, peer copies otherwise) and land in the
+ * outputs in input order (same bits as one bzr_trace_chain over all rays).  A one-frame bzr_tiled plan
+ * (below) created and destroyed per call: host pointers, or with BZR_DEVICE_PTRS rays and outputs on
+ * ctxs[0]'s device.  Synchronous either way; the mode / pipeline flags pass through.  Callers tracing
+ * many frames keep a plan instead (the RCCL communicator and the buffers are set up once). */
 bzr_status bzr_trace_tiled(bzr_ctx *const *ctxs, uint32_t nctx, const bzr_mesh *const *lenses,
                            const float *refractive_index, uint32_t nlens, const float *rays_soa, uint32_t n,
                            uint32_t tile_rays, float *out_rays_soa, uint32_t *out_status,
                            uint32_t *out_segments, uint32_t flags);
+
+/* ---- multi-GPU frames from one process, gathered on the device (one host thread drives
+ * every device, ncclCommInitAll, grouped ncclSend / ncclRecv to device 0) ---- */
+typedef struct bzr_tiled bzr_tiled;
+enum { BZR_GATHER_AUTO = 0, BZR_GATHER_RCCL = 1, BZR_GATHER_PEER = 2 };
+/* A frame plan over ndev devices and nslot frame slots: ctxs[s * ndev + d] is slot s's context on list
+ * device d (every slot lists the same devices in the same order; all contexts distinct).  The frame is n
+ * rays in tile-major order; device d traces tiles d, d + ndev, ... (its share).  The plan owns each
+ * device's share buffers per slot and device 0's receive buffers.  transport: BZR_GATHER_RCCL (one RCCL
+ * communicator per device, ncclCommInitAll; needs distinct devices), BZR_GATHER_PEER (hipMemcpyPeerAsync;
+ * any device list, including several list entries on one device), BZR_GATHER_AUTO (RCCL when the devices
+ * are distinct).  Not thread-safe; the contexts must not be used by other threads meanwhile. */
+bzr_status bzr_tiled_create(bzr_ctx *const *ctxs, uint32_t ndev, uint32_t nslot, uint32_t n, uint32_t tile_rays,
+                            int32_t transport, bzr_tiled **out);
+bzr_status bzr_tiled_destroy(bzr_tiled *plan);
+/* transport chosen; share_rays[ndev] (may be NULL): rays per device; npad (may be NULL): columns of a
+ * packed share (the largest share, in whole tiles) -- each device sends 28 * npad bytes per frame. */
+bzr_status bzr_tiled_info(const bzr_tiled *plan, int32_t *transport, uint32_t *share_rays, uint32_t *npad);
+/* The frame's input rays [6][n] (host memory, or with BZR_DEVICE_PTRS ctxs[0]'s device memory) into every
+ * device's share; synchronous.  They stay resident for every following frame. */
+bzr_status bzr_tiled_set_rays(bzr_tiled *plan, const float *rays_soa, uint32_t flags);
+/* Device d's share input [6][share_rays[d]] (device memory on device d), for callers that generate rays
+ * on the devices: write it (ordered before the next bzr_tiled_trace, e.g. then bzr_tiled_sync). */
+bzr_status bzr_tiled_share_rays(bzr_tiled *plan, uint32_t device_index, float **rays_soa);
+/* One frame on slot (frame number mod nslot): every device traces its share through
+ * lenses[d * nlens + l] (refract(INSIDE) then refract(OUTSIDE) per lens, as bzr_trace_chain), packs it
+ * (28 B per ray), the packed shares are gathered to device 0, which writes out_rays_soa [6][n],
+ * out_status [n] and out_segments [n] (may be NULL) in input order.  BZR_DEVICE_PTRS: outputs on ctxs[0]'s
+ * device; the call returns once the frame is queued (no host wait), frames on different slots overlap,
+ * and the outputs are ready on bzr_tiled_stream's stream (or after bzr_tiled_sync) -- keep one set of
+ * outputs per frame in flight.  Host pointers: synchronous.  Mode / pipeline flags pass through. */
+bzr_status bzr_tiled_trace(bzr_tiled *plan, const bzr_mesh *const *lenses, const float *refractive_index,
+                           uint32_t nlens, float *out_rays_soa, uint32_t *out_status, uint32_t *out_segments,
+                           uint32_t flags);
+/* Device 0's gather stream: the outputs of the last bzr_tiled_trace are complete in its order. */
+bzr_status bzr_tiled_stream(bzr_tiled *plan, void **hip_stream);
+bzr_status bzr_tiled_sync(bzr_tiled *plan);
 /* BezierMesh::interpolate(divisor) on the device (reference/bezierMesh.cpp:55-66): the tessellated
  * surface, divisor^2 sub-triangles of every patch, in the reference's order (sub-triangle outer,
  * patch inner).  out_xyz: divisor^2 * n_patches triangles x 3 vertices x 3 floats.  divisor >= 1.

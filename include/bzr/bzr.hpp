@@ -11,9 +11,10 @@
 //     uses for fixed-size float 3-vectors (redux a0 + (a1 + a2), cofactor inverse,
 //     normalized() = v / sqrt(|v|^2) guarded by |v|^2 > 0);
 //   * the ray-tracing hot path (BezierTriangle::intersect, BezierMesh::intersect,
-//     BezierLens::refract) runs on the GPU through libbzr's C ABI (include/bzr.h);
-//     the single-ray methods are batches of one, the batch overloads are the
-//     throughput interface.  There is no CPU implementation of the hot path here;
+//     BezierLens::refract): the batch overloads, bzr::traceChain and the multi-device
+//     calls run on the GPU through libbzr's C ABI (include/bzr.h) -- the throughput
+//     interface; the reference's single-ray methods run the same arithmetic on the
+//     host (one ray: no launch, no PCIe round trip), bit-identical to the batch path;
 //   * preprocessing (Mesh, BezierMesh construction) is host C++ as in the reference.
 #ifndef BZR_BZR_HPP
 #define BZR_BZR_HPP
@@ -357,7 +358,7 @@ class BezierTriangle final {  // cubic Bezier triangle; layout == bzr_patch (264
   Vertex interpolate(Vertex const &b) const { return interpolate(b(0), b(1), b(2)); }
   Vertex interpolateAboveOriginalCentroid() const { return mControlPoints[2]; }
   Vector getNormal(Vector const &barycentric) const;
-  // GPU (a batch of one); see BezierMesh::intersect for the batch interface.
+  // Host, bit-identical to the GPU (bzr_patch_intersect); see BezierMesh::intersect for the batch interface.
   BezierIntersection intersect(Ray const &ray, LimitPlaneIntersection limit) const;
 
   Plane mUnderlyingPlane;
@@ -406,7 +407,8 @@ class BezierMesh final {
   Mesh interpolate(int32_t divisor) const;
   std::vector<Vertex> dumpControlPoints() const;
   Mesh splitThickBezierTriangles() const;
-  BezierIntersection intersect(Ray const &ray) const;  // GPU, batch of one
+  BezierIntersection intersect(Ray const &ray) const;  // host (brute force, index order), bit-identical to the GPU
+  BezierIntersection intersect(Ray const &ray, uint32_t *patchIndex) const;  // the same + the patch hit (~0u: miss)
   // Batch interface (GPU).  patchIndex (optional) receives the index of the patch hit, ~0u on a miss.
   void intersect(Ray const *rays, std::size_t n, BezierIntersection *out, uint32_t *patchIndex = nullptr,
                  bzr::Context *ctx = nullptr) const;
@@ -426,7 +428,7 @@ class BezierLens final {
  public:
   BezierLens(float ri, BezierMesh const &mesh) : mRefractiveIndex(ri), mMesh(mesh) {}
   BezierLens(float ri, BezierMesh &&mesh) : mRefractiveIndex(ri), mMesh(std::move(mesh)) {}
-  std::pair<Ray, RefractionResult> refract(Ray const &ray, RefractionResult expected) const;  // GPU, batch of one
+  std::pair<Ray, RefractionResult> refract(Ray const &ray, RefractionResult expected) const;  // host, as intersect(Ray)
   void refract(Ray const *rays, RefractionResult const *expected, std::size_t n, Ray *outRays,
                RefractionResult *outStatus, bzr::Context *ctx = nullptr) const;
   float getRefractiveIndex() const { return mRefractiveIndex; }
@@ -446,6 +448,31 @@ void traceChain(std::vector<BezierLens const *> const &lenses, Ray const *rays, 
 void traceChainTiled(std::vector<Context *> const &ctxs, std::vector<BezierLens const *> const &lenses,
                      Ray const *rays, std::size_t n, Ray *outRays, RefractionResult *outStatus,
                      uint32_t *outSegments = nullptr, uint32_t tileRays = 4096);
+// Frame after frame over several devices from one process (bzr_tiled): slots[s][d] is frame slot s's
+// context on device d; a frame's n tile-major rays are dealt in tiles of tileRays to the devices and the
+// results gathered to device 0 on the device side (RCCL over xGMI between distinct devices, peer copies
+// otherwise).  The device-pointer trace() is asynchronous (frames on different slots overlap; keep one set
+// of outputs per frame in flight, sync() before reading them); the host-pointer trace() is synchronous.
+class TiledChain {
+ public:
+  TiledChain(std::vector<std::vector<Context *>> const &slots, std::vector<BezierLens const *> const &lenses,
+             std::size_t n, uint32_t tileRays = 4096, int transport = BZR_GATHER_AUTO);
+  ~TiledChain();
+  TiledChain(TiledChain const &) = delete;
+  TiledChain &operator=(TiledChain const &) = delete;
+  int transport() const;                                  // BZR_GATHER_RCCL or BZR_GATHER_PEER
+  void setRays(Ray const *rays);                          // n host rays, tile-major; stay resident
+  void setRaysDevice(float const *raysSoaOnDevice0);      // [6][n] SoA on slot 0 device 0
+  void trace(float *outRaysSoa, uint32_t *outStatus, uint32_t *outSegments = nullptr, uint32_t flags = 0);  // device 0
+  void trace(Ray *outRays, RefractionResult *outStatus, uint32_t *outSegments = nullptr, uint32_t flags = 0);  // host
+  void sync();
+
+ private:
+  bzr_tiled *mPlan = nullptr;
+  std::size_t mDevices = 0, mN = 0;
+  std::vector<bzr_mesh const *> mMeshes;  // [device][lens]
+  std::vector<float> mRi;
+};
 }  // namespace bzr
 
 static_assert(sizeof(BezierTriangle) == sizeof(bzr_patch), "BezierTriangle must match the 264-byte record");

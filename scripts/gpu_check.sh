@@ -1,10 +1,17 @@
 #!/bin/bash
-# GPU-box check: parity tests, smoke, bench, rocprof.  Ordinary failures (exit 1) continue to the
-# next step; a timeout, abort, segfault or signal stops the script (nothing more touches the GPU).
-# Env: STEPS="pytest smoke bench prof" selects steps; BENCH_ARGS / PROF_ARGS pass bench flags.
+# GPU-box check: the one entry point for GPU runs (rounds 1-3's one-off scripts/r03*_check*.sh were folded
+# into these steps; git history keeps them).  Ordinary failures (exit 1) continue to the next step; a
+# timeout, abort, segfault or signal stops the script (nothing more touches the GPU).
+# Env:
+#   STEPS="pytest smoke bench ..." selects steps (default: pytest smoke bench prof)
+#   RUN=name       output directory gpurun_out/$RUN (default gpurun_out)
+#   BENCH_ARGS     bench.py flags of the bench / rehearse2 steps
+#   PYTEST_ARGS    extra pytest args (e.g. -k pattern, a test file) of the pytest step
+#   PROF_TAG, PROF_BENCH, PROF_WORKLOAD   the prof step: scripts/prof_run.sh (kernel trace + PMC passes)
+#   AB_ARGS        the ab step: scripts/ab.py arguments
 R="$GRAFT_REPO_ROOT"
 cd "$R" || exit 2
-OUT="$R/gpurun_out"
+OUT="$R/gpurun_out/${RUN:-.}"
 mkdir -p "$OUT"
 STEPS=${STEPS:-"pytest smoke bench prof"}
 step() {  # step <name> <seconds> <cmd...>
@@ -19,15 +26,16 @@ step() {  # step <name> <seconds> <cmd...>
 nproc > "$OUT/host.txt"; lscpu | grep -m1 "Model name" >> "$OUT/host.txt"
 for s in $STEPS; do
   case $s in
-    pytest) step pytest_gpu 900 python -u -m pytest tests -x -v -m gpu -p no:cacheprovider --timeout 120 --timeout-method thread ;;
+    pytest) step pytest_gpu 900 python -u -m pytest tests -x -v -m gpu -p no:cacheprovider --timeout 120 \
+              --timeout-method thread ${PYTEST_ARGS:-} ;;
     smoke)  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)  step bench 600 python bench.py ${BENCH_ARGS:-} ;;
-    prof)   (cd /tmp && export TMPDIR=/tmp && step prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run \
-               -- python3 "$R/bench.py" --steps 10 --warmup 2 --cpu-baseline off ${PROF_ARGS:-}) || exit $? ;;
-    pmc)    (cd /tmp && export TMPDIR=/tmp && \
-             step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_fetch" -o run \
-               -- python3 "$R/bench.py" --steps 3 --warmup 1 --cpu-baseline off ${PROF_ARGS:-} && \
-             step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc_write" -o run \
-               -- python3 "$R/bench.py" --steps 3 --warmup 1 --cpu-baseline off ${PROF_ARGS:-}) || exit $? ;;
+    # 2 ranks on the box's one GPU, launched by bench.py itself (no torch.distributed.run): gloo, every rank
+    # on device 0 (RCCL refuses two ranks on one device).  Exercises the launcher, the tile deal and the
+    # per-frame gather; not a scaling measurement.
+    rehearse2) BZR_BENCH_BACKEND=gloo BZR_BENCH_DEVICE=0 step rehearse2 300 python bench.py --gpus 2 --steps 5 \
+              --warmup 2 --cpu-baseline off ${BENCH_ARGS:-} ;;
+    prof)   TAG=${PROF_TAG:-prof} BENCH=${PROF_BENCH:-} WORKLOAD=${PROF_WORKLOAD:-} step prof 1500 bash scripts/prof_run.sh ;;
+    ab)     step ab 900 python scripts/ab.py ${AB_ARGS:-} ;;
   esac
 done

@@ -3,9 +3,12 @@
 // It includes the reference's header names (include/bzr/*.h) and uses the reference's API the way
 // reference/test.cpp and reference/googleTest.cpp do.  Part 1 restates the googleTest L1 cases
 // (reference/googleTest.cpp:46-353, cgEpsilon = 1e-4) on the product's value types; part 2 runs the
-// host preprocessing API; part 3 (only with a HIP device) runs BezierMesh::intersect,
-// BezierTriangle::intersect and BezierLens::refract through libbzr and checks them bit-for-bit against
-// the oracle (test infrastructure, linked only into this test program).
+// host preprocessing API; part 3 runs the single-ray BezierMesh::intersect, BezierTriangle::intersect and
+// BezierLens::refract (host arithmetic of the product, single_ray.cpp) against the oracle (test
+// infrastructure, linked only into this test program); part 4 (only with a HIP device) runs the batch
+// overloads, the chain and the multi-device calls through libbzr and checks them bit-for-bit against the
+// single-ray results and the oracle, and times one ray through each path.
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -137,35 +140,57 @@ static void preprocessing(Mesh &lens) {
   orc_mesh_free(&om);
 }
 
-static void hot_path(Mesh const &lensMesh) {
+static bool same_hit(BezierIntersection const &a, BezierIntersection const &b) {
+  return a.mWhat == b.mWhat && a.mIntersection.mValid == b.mIntersection.mValid &&
+         std::memcmp(&a.mIntersection.mDistance, &b.mIntersection.mDistance, 4) == 0 &&
+         std::memcmp(&a.mIntersection.mCosIncidence, &b.mIntersection.mCosIncidence, 4) == 0 &&
+         std::memcmp(a.mIntersection.mPoint.data(), b.mIntersection.mPoint.data(), 12) == 0 &&
+         std::memcmp(a.mBarycentric.data(), b.mBarycentric.data(), 12) == 0 &&
+         std::memcmp(a.mNormal.data(), b.mNormal.data(), 12) == 0;
+}
+static bool same_ray(Ray const &a, Ray const &b) {
+  return std::memcmp(a.mStart.data(), b.mStart.data(), 12) == 0 && std::memcmp(a.mDirection.data(), b.mDirection.data(), 12) == 0;
+}
+
+// cfg2's primary rays: plane x = 0, y in [-4.2, 4.2], z in [-2.1, 2.1], along +x
+static std::vector<Ray> cfg2_rays(int side) {
+  std::vector<Ray> rays;
+  for (int i = 0; i < side; ++i)
+    for (int j = 0; j < side; ++j)
+      rays.emplace_back(Vertex{0.0f, -4.2f + 8.4f * (j + 0.5f) / side, -2.1f + 4.2f * (i + 0.5f) / side}, Vector{1, 0, 0});
+  return rays;
+}
+
+template <typename F>
+static double us_per_call(F &&f, int calls) {
+  auto t0 = std::chrono::steady_clock::now();
+  for (int k = 0; k < calls; ++k) f(k);
+  return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() / calls;
+}
+
+// Part 3: the reference's single-ray calls (reference/test.cpp:268,281,380), on the host, vs the oracle.
+static void single_ray(Mesh const &lensMesh) {
   BezierMesh bezier(lensMesh);
   std::vector<opatch> op(bezier.size());
   std::memcpy(op.data(), &bezier[0], sizeof(opatch) * op.size());
   BezierLens lens(1.3f, bezier);
-  // a small image, single-ray calls like reference/test.cpp:376-401, and the batch overloads
-  std::vector<Ray> rays;
-  for (int i = 0; i < 24; ++i)
-    for (int j = 0; j < 24; ++j)
-      rays.emplace_back(Vertex{0.0f, -4.2f + 8.4f * (j + 0.5f) / 24, -2.1f + 4.2f * (i + 0.5f) / 24}, Vector{1, 0, 0});
+  std::vector<Ray> rays = cfg2_rays(24);
   int hits = 0, exits = 0;
-  std::vector<BezierIntersection> batch(rays.size());
-  std::vector<uint32_t> patch(rays.size());
-  bezier.intersect(rays.data(), rays.size(), batch.data(), patch.data());
   for (std::size_t r = 0; r < rays.size(); ++r) {
     oray orr{ov3{rays[r].mStart(0), rays[r].mStart(1), rays[r].mStart(2)},
              ov3{rays[r].mDirection(0), rays[r].mDirection(1), rays[r].mDirection(2)}};
     ohit want = orc_mesh_intersect(op.data(), op.size(), &orr);
-    BezierIntersection got = r % 37 == 0 ? bezier.intersect(rays[r]) : batch[r];
+    BezierIntersection got = bezier.intersect(rays[r]);
     CHECK(static_cast<uint32_t>(got.mWhat) == want.what);
     if (want.what == ORC_INTERSECT) {
       ++hits;
-      CHECK(patch[r] == want.patch);
       CHECK(std::memcmp(&got.mIntersection.mDistance, &want.t, 4) == 0);
       CHECK(std::memcmp(got.mBarycentric.data(), &want.bary, 12) == 0);
       CHECK(std::memcmp(got.mNormal.data(), &want.normal, 12) == 0);
       // the single-patch API gives the same hit for the winning patch
-      BezierIntersection one = bezier[patch[r]].intersect(rays[r], BezierTriangle::LimitPlaneIntersection::cNone);
+      BezierIntersection one = bezier[want.patch].intersect(rays[r], BezierTriangle::LimitPlaneIntersection::cNone);
       CHECK(one.mWhat == BezierIntersection::What::cIntersect);
+      CHECK(std::memcmp(&one.mIntersection.mDistance, &want.t, 4) == 0);
     }
     Ray cur = rays[r];
     RefractionResult st = RefractionResult::cNone;
@@ -177,6 +202,7 @@ static void hot_path(Mesh const &lensMesh) {
       CHECK(static_cast<uint32_t>(res.second) == ost);
       st = res.second;
       if (st == RefractionResult::cNone) break;
+      CHECK(std::memcmp(res.first.mStart.data(), &oo.start, 12) == 0);
       CHECK(std::memcmp(res.first.mDirection.data(), &oo.dir, 12) == 0);
       cur = res.first;
       orr = oo;
@@ -184,23 +210,119 @@ static void hot_path(Mesh const &lensMesh) {
     exits += st == RefractionResult::cOutside;
   }
   CHECK(hits > 150 && exits > 100);
+  std::printf("single ray (host): %d hits, %d exits of %zu rays\n", hits, exits, rays.size());
+}
+
+// Part 4: the GPU batch paths vs the host single-ray path, bit for bit, and the per-call latency of both.
+static void hot_path(Mesh const &lensMesh) {
+  BezierMesh bezier(lensMesh);
+  BezierLens lens(1.3f, bezier);
+  std::vector<Ray> rays = cfg2_rays(64);
+  const std::size_t n = rays.size();
+  // BezierMesh::intersect: GPU batch == host single ray, every field and the patch index
+  std::vector<BezierIntersection> batch(n);
+  std::vector<uint32_t> patch(n);
+  bezier.intersect(rays.data(), n, batch.data(), patch.data());
+  int hits = 0, same = 0;
+  for (std::size_t r = 0; r < n; ++r) {
+    uint32_t hp = 0;
+    BezierIntersection one = bezier.intersect(rays[r], &hp);
+    same += same_hit(one, batch[r]) && hp == patch[r];
+    hits += batch[r].mWhat == BezierIntersection::What::cIntersect;
+  }
+  CHECK(same == static_cast<int>(n));
+  CHECK(hits > 1000);
+  // BezierTriangle::intersect: host vs bzr_patch_intersect, both limits, for every ray's winning (or first) patch
+  {
+    std::vector<uint32_t> idx(n), lim(n);
+    std::vector<float> soa(6 * n), h(13 * n);
+    for (std::size_t r = 0; r < n; ++r) {
+      idx[r] = patch[r] == 0xFFFFFFFFu ? static_cast<uint32_t>(r % bezier.size()) : patch[r];
+      lim[r] = static_cast<uint32_t>(r & 1u);
+      for (int k = 0; k < 3; ++k) {
+        soa[k * n + r] = rays[r].mStart(k);
+        soa[(3 + k) * n + r] = rays[r].mDirection(k);
+      }
+    }
+    bzr::Context &c = bzr::defaultContext();
+    bzr::check(bzr_patch_intersect(c.get(), bezier.device(c), idx.data(), lim.data(), soa.data(), static_cast<uint32_t>(n),
+                                   h.data(), BZR_HOST_PTRS));
+    int agree = 0;
+    for (std::size_t r = 0; r < n; ++r) {
+      BezierIntersection one = bezier[idx[r]].intersect(rays[r], static_cast<BezierTriangle::LimitPlaneIntersection>(lim[r]));
+      uint32_t what;
+      std::memcpy(&what, &h[11 * n + r], 4);
+      agree += static_cast<uint32_t>(one.mWhat) == what && std::memcmp(&one.mIntersection.mDistance, &h[r], 4) == 0 &&
+               std::memcmp(one.mBarycentric.data(), &h[5 * n + r], 4) == 0 &&
+               std::memcmp(one.mBarycentric.data() + 1, &h[6 * n + r], 4) == 0 &&
+               std::memcmp(one.mBarycentric.data() + 2, &h[7 * n + r], 4) == 0 &&
+               std::memcmp(one.mNormal.data(), &h[8 * n + r], 4) == 0;
+    }
+    CHECK(agree == static_cast<int>(n));
+  }
+  // BezierLens::refract: GPU batch == host single ray (both steps of the chain)
+  std::vector<Ray> cur = rays, next(n);
+  std::vector<RefractionResult> expect(n, RefractionResult::cInside), st(n);
+  int refr_same = 0, exits = 0;
+  for (uint32_t j = 0; j < 2u; ++j) {
+    std::fill(expect.begin(), expect.end(), j == 0 ? RefractionResult::cInside : RefractionResult::cOutside);
+    lens.refract(cur.data(), expect.data(), n, next.data(), st.data());
+    for (std::size_t r = 0; r < n; ++r) {
+      auto one = lens.refract(cur[r], expect[r]);
+      refr_same += one.second == st[r] && same_ray(one.first, next[r]);
+      if (j == 1) exits += st[r] == RefractionResult::cOutside;
+    }
+    cur = next;
+  }
+  CHECK(refr_same == static_cast<int>(2 * n));
   // the whole chain in one call
-  std::vector<Ray> out(rays.size());
-  std::vector<RefractionResult> status(rays.size());
-  std::vector<uint32_t> seg(rays.size());
-  bzr::traceChain({&lens}, rays.data(), rays.size(), out.data(), status.data(), seg.data());
+  std::vector<Ray> out(n);
+  std::vector<RefractionResult> status(n);
+  std::vector<uint32_t> seg(n);
+  bzr::traceChain({&lens}, rays.data(), n, out.data(), status.data(), seg.data());
   int chainExits = 0;
   for (auto s : status) chainExits += s == RefractionResult::cOutside;
-  CHECK(chainExits == exits);
-  // the same chain dealt over two contexts (two streams / host threads on device 0), tiles of 100 rays
+  CHECK(chainExits > 0);
+  // the same chain dealt over two contexts on device 0, gathered on the device (peer path), tiles of 100 rays
   bzr::Context c0(0), c1(0);
-  std::vector<Ray> outT(rays.size());
-  std::vector<RefractionResult> statusT(rays.size());
-  std::vector<uint32_t> segT(rays.size());
-  bzr::traceChainTiled({&c0, &c1}, {&lens}, rays.data(), rays.size(), outT.data(), statusT.data(), segT.data(), 100);
+  std::vector<Ray> outT(n);
+  std::vector<RefractionResult> statusT(n);
+  std::vector<uint32_t> segT(n);
+  bzr::traceChainTiled({&c0, &c1}, {&lens}, rays.data(), n, outT.data(), statusT.data(), segT.data(), 100);
   CHECK(statusT == status && segT == seg);
   CHECK(std::memcmp(outT.data(), out.data(), out.size() * sizeof(Ray)) == 0);
-  std::printf("hot path: %d hits, %d exits of %zu rays\n", hits, exits, rays.size());
+  // frame after frame: a TiledChain plan, 2 slots x 2 contexts on device 0, host outputs
+  {
+    bzr::Context s00(0), s01(0), s10(0), s11(0);
+    bzr::TiledChain frames({{&s00, &s01}, {&s10, &s11}}, {&lens}, n, 512);
+    CHECK(frames.transport() == BZR_GATHER_PEER);
+    frames.setRays(rays.data());
+    for (int k = 0; k < 3; ++k) {
+      std::vector<Ray> o(n);
+      std::vector<RefractionResult> so(n);
+      std::vector<uint32_t> sg(n);
+      frames.trace(o.data(), so.data(), sg.data());
+      CHECK(so == status && sg == seg);
+      CHECK(std::memcmp(o.data(), out.data(), out.size() * sizeof(Ray)) == 0);
+    }
+  }
+  // per-call latency of one ray: host single-ray methods vs the GPU batch of one (launch + PCIe + sync)
+  const int calls = 200;
+  BezierIntersection sink;
+  double host_mesh = us_per_call([&](int k) { sink = bezier.intersect(rays[(k * 97) % n]); }, calls);
+  double gpu_mesh = us_per_call([&](int k) { bezier.intersect(&rays[(k * 97) % n], 1, &sink); }, calls);
+  double host_patch = us_per_call([&](int k) {
+    sink = bezier[patch[(k * 97) % n] % bezier.size()].intersect(rays[(k * 97) % n], BezierTriangle::LimitPlaneIntersection::cThis);
+  }, calls);
+  std::pair<Ray, RefractionResult> rsink;
+  double host_refr = us_per_call([&](int k) { rsink = lens.refract(rays[(k * 97) % n], RefractionResult::cInside); }, calls);
+  RefractionResult e1 = RefractionResult::cInside, s1;
+  Ray o1;
+  double gpu_refr = us_per_call([&](int k) { lens.refract(&rays[(k * 97) % n], &e1, 1, &o1, &s1); }, calls);
+  std::printf("latency us/call (cfg2 lens, %zu patches): BezierMesh::intersect host %.2f gpu-batch-of-1 %.2f; "
+              "BezierTriangle::intersect host %.3f; BezierLens::refract host %.2f gpu-batch-of-1 %.2f\n",
+              bezier.size(), host_mesh, gpu_mesh, host_patch, host_refr, gpu_refr);
+  std::printf("hot path: %d hits, %d exits of %zu rays (GPU batch == host single ray)\n", hits, exits, n);
 }
 
 // UniformHemisphere (reference/hostUtil.cpp) through the drop-in header vs the oracle's restatement of
@@ -230,6 +352,7 @@ int main() {
   preprocessing(lens);
   int32_t devices = 0;
   bzr_device_count(&devices);
+  single_ray(lens);
   if (devices > 0) hot_path(lens);
   else std::printf("no HIP device: hot-path part skipped\n");
   std::printf("%d checks, %d failed\n", g_checks, g_fail);

@@ -88,8 +88,26 @@ def test_trace_tiled_validates_before_touching_a_device(bzr):
     one = (ctypes.c_void_p * 1)(1)
     assert L.bzr_trace_tiled(one, 1, one, f, 1, None, 0, 0, None, None, None, 0) == 1
     assert b"tile_rays" in L.bzr_last_error()
-    assert L.bzr_trace_tiled(one, 1, one, f, 1, None, 0, 64, None, None, None, bzr.DEVICE_PTRS) == 1
-    assert b"host pointers" in L.bzr_last_error()
+    assert L.bzr_trace_tiled(one, 1, one, f, 1, None, 64, 64, None, None, None, bzr.DEVICE_PTRS) == 1
+    assert b"null buffer" in L.bzr_last_error()
+
+
+def test_tiled_plan_validates_before_touching_a_device(bzr):
+    """bzr_tiled_create / _trace / _info reject bad arguments without a device (include/bzr.h)."""
+    import ctypes
+    L = bzr.lib()
+    out = ctypes.c_void_p()
+    one = (ctypes.c_void_p * 1)(1)
+    assert L.bzr_tiled_create(None, 0, 1, 64, 64, 0, ctypes.byref(out)) == 1 and b"no contexts" in L.bzr_last_error()
+    assert L.bzr_tiled_create(one, 1, 1, 64, 0, 0, ctypes.byref(out)) == 1 and b"tile_rays" in L.bzr_last_error()
+    assert L.bzr_tiled_create(one, 1, 1, 0, 64, 0, ctypes.byref(out)) == 1 and b"empty frame" in L.bzr_last_error()
+    assert L.bzr_tiled_create(one, 1, 1, 64, 64, 7, ctypes.byref(out)) == 1 and b"transport" in L.bzr_last_error()
+    two = (ctypes.c_void_p * 2)(1, 1)
+    assert L.bzr_tiled_create(two, 1, 2, 64, 64, 0, ctypes.byref(out)) == 1 and b"repeated" in L.bzr_last_error()
+    assert out.value is None
+    assert L.bzr_tiled_trace(None, None, None, 0, None, None, None, 0) == 1
+    assert L.bzr_tiled_info(None, None, None, None) == 1
+    assert L.bzr_tiled_destroy(None) == 0
 
 
 def test_patch_records_view_as_reference_struct(bzr):

@@ -1,9 +1,9 @@
 """bzr_trace_tiled: the refraction chain dealt over several contexts from one process.
 
 The GPU box has one device, so the multi-device path runs with two and three contexts on device 0
-(separate streams, separate host threads): the tile dealing, packing and scatter-back are the same
-code as across 8 devices.  The bar is bit-identity with one bzr_trace_chain over all rays, which
-tests/test_gpu_parity.py pins to the oracle.
+(separate streams): the tile dealing, per-device packing, device-side gather (peer copies; RCCL with a
+one-device communicator) and the unpack on device 0 are the same code as across 8 devices.  The bar is
+bit-identity with one bzr_trace_chain over all rays, which tests/test_gpu_parity.py pins to the oracle.
 """
 import numpy as np
 import pytest
@@ -37,3 +37,97 @@ def test_tiled_fast_mode_passes_through(bzr, ctx):
     got = bzr.trace_tiled(ctxs, [[bzr.DeviceMesh(c, patches)] for c in ctxs], [1.3], rays, mode=bzr.MODE_FAST)
     for g, w in zip(got, want):
         assert np.array_equal(np.asarray(g).view(np.uint32), np.asarray(w).view(np.uint32))
+
+
+def _cfg4(bzr):
+    cfg = CONFIGS["cfg4"]
+    patches = [build_lens(bzr.TriMesh, lens).bezier_patches() for lens in cfg.lenses]
+    return cfg, patches, [lens.ri for lens in cfg.lenses]
+
+
+def _same(got, want):
+    for g, w in zip(got, want):
+        g = g.cpu().numpy() if hasattr(g, "cpu") else np.asarray(g)
+        w = w.cpu().numpy() if hasattr(w, "cpu") else np.asarray(w)
+        assert np.array_equal(g.view(np.uint32), w.view(np.uint32))
+
+
+def test_tiled_device_pointers_equal_single_chain(bzr, ctx):
+    """bzr_trace_tiled with BZR_DEVICE_PTRS: rays and outputs on device 0, the gather on the device."""
+    import torch
+
+    cfg, patches, ri = _cfg4(bzr)
+    rays = grid_rays(cfg, side=256)
+    want = bzr.trace_chain(ctx, [bzr.DeviceMesh(ctx, p) for p in patches], ri, rays)
+    ctxs = [bzr.Context(0) for _ in range(3)]
+    got = bzr.trace_tiled(ctxs, [[bzr.DeviceMesh(c, p) for p in patches] for c in ctxs], ri,
+                          torch.from_numpy(rays).cuda(), tile_rays=4096)
+    assert got[0].is_cuda
+    _same(got, want)
+
+
+@pytest.mark.parametrize("transport,ndev", [("peer", 1), ("peer", 2), ("peer", 3), ("rccl", 1), ("auto", 1)])
+def test_tiled_plan_frames_in_flight(bzr, ctx, transport, ndev):
+    """A bzr_tiled plan over `ndev` list devices (all device 0 on this box: the peer path; the RCCL path is
+    the world-size-1 communicator with its self send/recv), 2 slots, 5 frames queued back to back with a
+    different refractive index per frame: each frame's device-0 outputs equal one bzr_trace_chain with
+    that index, so a slot buffer reused before its gather completed would fail."""
+    import torch
+
+    cfg, patches, _ = _cfg4(bzr)
+    rays = grid_rays(cfg, side=256)
+    n = rays.shape[1]
+    tp = {"peer": bzr.GATHER_PEER, "rccl": bzr.GATHER_RCCL, "auto": bzr.GATHER_AUTO}[transport]
+    slots = [[bzr.Context(0) for _ in range(ndev)] for _ in range(2)]
+    lenses = [[bzr.DeviceMesh(c, p) for p in patches] for c in slots[0]]  # device d's copy (same device here)
+    plan = bzr.TiledPlan(slots, n, tile_rays=4096, transport=tp)
+    got_tp, share, npad = plan.info()
+    assert got_tp == (bzr.GATHER_RCCL if transport in ("rccl", "auto") else bzr.GATHER_PEER)
+    assert int(share.sum()) == n and npad == -(-16 // ndev) * 4096
+    plan.set_rays(torch.from_numpy(rays).cuda())
+    ris = [1.3, 1.45, 1.2, 1.6, 1.3]
+    outs = [(torch.empty((6, n), device="cuda"), torch.empty(n, dtype=torch.int32, device="cuda"),
+             torch.empty(n, dtype=torch.int32, device="cuda")) for _ in ris]
+    for r, o in zip(ris, outs):
+        plan.trace(lenses, [r, r], *o)
+    plan.sync()
+    single = [bzr.DeviceMesh(ctx, p) for p in patches]
+    for r, o in zip(ris, outs):
+        _same(o, bzr.trace_chain(ctx, single, [r, r], rays))
+    plan.close()
+
+
+class _DevArray:
+    """A raw device pointer as a torch-viewable array (__cuda_array_interface__, no copy)."""
+
+    def __init__(self, ptr, shape):
+        self.__cuda_array_interface__ = {"shape": shape, "typestr": "<f4", "data": (ptr, False), "version": 2,
+                                         "strides": None}
+
+
+def test_tiled_plan_share_rays_and_host_outputs(bzr, ctx):
+    """Rays written straight into each device's share (bzr_tiled_share_rays), host-pointer outputs, a
+    ragged last tile (n not a multiple of tile_rays)."""
+    import ctypes
+
+    import torch
+
+    cfg, patches, ri = _cfg4(bzr)
+    rays = grid_rays(cfg, side=256)[:, :60000].copy()
+    n, tile = rays.shape[1], 1000
+    slots = [[bzr.Context(0) for _ in range(3)]]
+    plan = bzr.TiledPlan(slots, n, tile_rays=tile, transport=bzr.GATHER_PEER)
+    _, share, npad = plan.info()
+    assert npad == 20 * tile
+    for d in range(3):
+        cols = np.concatenate([np.arange(k * tile, min(n, (k + 1) * tile)) for k in range(d, -(-n // tile), 3)])
+        assert len(cols) == share[d]
+        p = ctypes.c_void_p()
+        bzr._check(bzr.lib().bzr_tiled_share_rays(plan.handle, d, ctypes.byref(p)))
+        view = torch.as_tensor(_DevArray(p.value, (6, int(share[d]))), device="cuda")
+        view.copy_(torch.from_numpy(np.ascontiguousarray(rays[:, cols])).cuda())
+    torch.cuda.synchronize()
+    out = (np.empty((6, n), np.float32), np.empty(n, np.uint32), np.empty(n, np.uint32))
+    lenses = [[bzr.DeviceMesh(c, p) for p in patches] for c in slots[0]]
+    plan.trace(lenses, ri, *out)
+    _same(out, bzr.trace_chain(ctx, [bzr.DeviceMesh(ctx, p) for p in patches], ri, rays))
