@@ -384,6 +384,15 @@ def pack_frame(ctx: Context, layout: str, rays, status, segments, packed, npad: 
     if layout not in PACK_LAYOUTS:
         raise ValueError(f"layout {layout!r}")
     n = int(status.shape[0])
+    if int(segments.shape[0]) != n:
+        raise BzrError(f"pack_frame: segments [{int(segments.shape[0])}] for status [{n}]")
+    if rays is not None and tuple(rays.shape) != (6, n):
+        raise BzrError(f"pack_frame: rays must be [6, {n}], got {tuple(rays.shape)}")
+    # the device writes this many floats into `packed` (include/bzr.h bzr_pack_frame)
+    need = {"image": npad, "rays": 7 * npad, "compact": npad // 4 + 1 + 6 * (cap + 1)}[layout]
+    if int(packed.numel()) < need:
+        raise BzrError(f"pack_frame: {layout} layout needs {need} floats (npad {npad}, cap {cap}), packed has "
+                       f"{int(packed.numel())}")
     bufs = [_Buf(status, np.uint32), _Buf(segments, np.uint32), _Buf(packed, np.float32, True)]
     r = _Buf(rays, np.float32) if rays is not None else _Buf(None, np.float32)
     if r.ptr is not None:

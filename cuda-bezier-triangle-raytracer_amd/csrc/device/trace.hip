@@ -2997,16 +2997,18 @@ extern "C" bzr_status bzr_mesh_interpolate(bzr_ctx *ctx, const bzr_mesh *mesh, i
 // ------------------------------------------------------------ illumination
 namespace {
 // Rays first .. first+n-1 of the emitter into rays [6][ld].  With `status`: rays that cannot meet the
-// first lens's bounding sphere start as NONE (culled, never traced), the others INSIDE (the chain's
-// first refraction expects to enter the lens); stats[EMITTED], stats[CULLED] count them.
+// first lens's bounding sphere (over its proven gate regions) and pass none of its always-listed patches'
+// planar gates start as NONE (culled, never traced), the others INSIDE (the chain's first refraction
+// expects to enter the lens); stats[EMITTED], stats[CULLED] count them.
 __global__ __launch_bounds__(kBlock) void k_emit(bzr_emitter em, BeltTable bt, uint64_t first, uint32_t n, uint32_t ld,
                                                  float *__restrict__ rays, uint32_t *__restrict__ patch,
                                                  uint32_t *__restrict__ status, uint32_t *__restrict__ segments,
-                                                 float4 sphere, unsigned long long *__restrict__ stats) {
+                                                 float4 sphere, const float4 *__restrict__ always, uint32_t n_always,
+                                                 unsigned long long *__restrict__ stats) {
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   bool culled = false;
+  f3 o = mk(0.0f, 0.0f, 0.0f), d = o;
   if (i < n) {
-    f3 o, d;
     uint32_t p;
     emit_ray(em, bt, first + i, o, d, p);
     store_ray(rays, ld, i, o, d);
@@ -3014,6 +3016,15 @@ __global__ __launch_bounds__(kBlock) void k_emit(bzr_emitter em, BeltTable bt, u
     if (status) {
       const float sp[4] = {sphere.x, sphere.y, sphere.z, sphere.w};
       culled = !may_hit_sphere(o, d, sp);
+    }
+  }
+  if (status) {
+    // the always list has no box inside the sphere: a ray outside it is kept if any of those gates passes
+    for (uint32_t k = 0; k < n_always && __any(culled); ++k) {
+      uint32_t b;
+      if (always_gate(always, k, culled, o, d, b)) culled = false;
+    }
+    if (i < n) {
       status[i] = culled ? BZR_RR_NONE : BZR_RR_INSIDE;
       if (segments) segments[i] = 0u;
     }
@@ -3121,7 +3132,7 @@ extern "C" bzr_status bzr_emit(bzr_ctx *ctx, const bzr_emitter *em, uint64_t fir
   uint32_t *d_patch = host ? (patch_index ? st.take<uint32_t>(n) : nullptr) : patch_index;
   hipLaunchKernelGGL(k_emit, dim3(grid_for(n)), dim3(kBlock), 0, ctx->stream, *em, bt, first, n, n, d_rays, d_patch,
                      (uint32_t *)nullptr, (uint32_t *)nullptr, make_float4(0.0f, 0.0f, 0.0f, 0.0f),
-                     (unsigned long long *)nullptr);
+                     (const float4 *)nullptr, 0u, (unsigned long long *)nullptr);
   BZR_HIP(hipGetLastError());
   if (host) {
     BZR_HIP(hipMemcpyAsync(rays_soa, d_rays, rb, hipMemcpyDeviceToHost, ctx->stream));
@@ -3190,7 +3201,7 @@ extern "C" bzr_status bzr_illuminate(bzr_ctx *ctx, const bzr_mesh *const *lenses
   for (uint64_t first = 0; first < total_rays; first += B) {
     const uint32_t m = (uint32_t)std::min<uint64_t>(B, total_rays - first);
     hipLaunchKernelGGL(k_emit, dim3(grid_for(m)), dim3(kBlock), 0, ctx->stream, *em, bt, first, m, B, d_rays,
-                       (uint32_t *)nullptr, d_st, d_seg, sphere, d_stats);
+                       (uint32_t *)nullptr, d_st, d_seg, sphere, set.lens[0].always, set.lens[0].n_always, d_stats);
     if (!staged) {  // the chain in place over the batch; culled rays (status NONE) are skipped
       TraceJob job{};
       job.rays = d_rays;

@@ -14,6 +14,7 @@
 #include "bvh.hpp"
 
 #include <algorithm>
+#include <exception>
 #include <cfloat>
 #include <array>
 #include <cmath>
@@ -816,14 +817,21 @@ Bvh build_bvh(const float *records, uint32_t n, uint32_t stride_words, int tier)
       fit_obb(region[p].pts, 2.0 * region[p].pad, &out.patch_obb[(size_t)p * 16]);  // always-hit if unbounded
       out.patch_obb[(size_t)p * 16 + 15] = 1.0f;
     }
-  ritter_sphere(box, out.sphere);
+  {  // the sphere over the tree's (proven) boxes only: the always list has no box (bzr_illuminate tests it
+     // behind the sphere per ray instead), so one unproven patch does not disable the cull
+    std::vector<Box> proven;
+    for (uint32_t p = 0; p < n; ++p)
+      if (region[p].proven) proven.push_back(box[p]);
+    ritter_sphere(proven, out.sphere);
+  }
   return out;
 }
 
 // Ritter's bounding sphere (the README's pre-cull, reference/README.md:194) over the corners of every
-// non-empty gate-region box: a ray that misses it cannot meet any gate region, so it passes no
-// planar gate.  Any non-finite corner disables the cull (radius +inf).  The radius is padded by
-// 1e-6 relative so the float-rounded centre and radius still enclose every corner.
+// non-empty gate-region box given (build_bvh: the proven ones): a ray that misses it cannot meet any of
+// those gate regions, so it passes none of their planar gates.  Any non-finite corner disables the cull
+// (radius +inf).  The radius is padded by 1e-6 relative so the float-rounded centre and radius still
+// enclose every corner.
 void ritter_sphere(std::vector<Box> const &box, float out[4]) {
   std::vector<std::array<double, 3>> pts;
   bool finite = true;
@@ -868,8 +876,10 @@ void ritter_sphere(std::vector<Box> const &box, float out[4]) {
 }  // namespace bzr_host
 
 // ---- debug / test entry point (include/bzr_debug.h) ----
+extern "C" void bzr_internal_set_error(const char *msg);
 extern "C" int32_t bzr_debug_gate_boxes_tier(const void *patches, uint32_t n, uint32_t stride, int32_t tier,
                                              float *boxes, float *s_max) {
+  try {
   if ((!patches && n) || (!boxes && n) || !s_max || stride % 4 || stride < 264) return 1;
   if (tier != bzr_host::kTierFar && tier != bzr_host::kTierNear) return 1;
   bzr_host::Bvh bvh = bzr_host::build_bvh(static_cast<const float *>(patches), n, stride / 4, tier);
@@ -882,6 +892,10 @@ extern "C" int32_t bzr_debug_gate_boxes_tier(const void *patches, uint32_t n, ui
   }
   *s_max = bvh.s_max;
   return 0;
+  } catch (std::exception const &e) {  // build_bvh's invariant checks: a status, not a throw across the C ABI
+    bzr_internal_set_error(e.what());
+    return 2;
+  }
 }
 
 extern "C" int32_t bzr_debug_gate_boxes(const void *patches, uint32_t n, uint32_t stride, float *boxes, float *s_max) {
@@ -925,15 +939,21 @@ bool obb_h(const float f[15], const float s[3], const float d[3]) {
 // Per patch (mesh order): its oriented gate-region box (c, u, v, w, h) and a flag word 1.0f when the patch
 // is in the wide subtree (the box its parent node tests), else 16 zeros.
 extern "C" int32_t bzr_debug_gate_obbs(const void *patches, uint32_t n, uint32_t stride, int32_t tier, float *out) {
+  try {
   if ((!patches && n) || (!out && n) || stride % 4 || stride < 264) return 1;
   if (tier != bzr_host::kTierFar && tier != bzr_host::kTierNear) return 1;
   bzr_host::Bvh bvh = bzr_host::build_bvh(static_cast<const float *>(patches), n, stride / 4, tier);
   std::memcpy(out, bvh.patch_obb.data(), (size_t)n * 16 * sizeof(float));
   return 0;
+  } catch (std::exception const &e) {  // build_bvh's invariant checks: a status, not a throw across the C ABI
+    bzr_internal_set_error(e.what());
+    return 2;
+  }
 }
 
 extern "C" int32_t bzr_debug_traverse(const void *patches, uint32_t n, uint32_t stride, const float *rays, uint32_t nr,
                                       uint8_t *hits, uint64_t stats[4]) {
+  try {
   if ((!patches && n) || (!rays && nr) || !stats || stride % 4 || stride < 264) return 1;
   bzr_host::Bvh far = bzr_host::build_bvh(static_cast<const float *>(patches), n, stride / 4, bzr_host::kTierFar);
   bzr_host::Bvh near = bzr_host::build_bvh(static_cast<const float *>(patches), n, stride / 4, bzr_host::kTierNear);
@@ -1000,6 +1020,10 @@ extern "C" int32_t bzr_debug_traverse(const void *patches, uint32_t n, uint32_t 
     }
   }
   return 0;
+  } catch (std::exception const &e) {  // build_bvh's invariant checks: a status, not a throw across the C ABI
+    bzr_internal_set_error(e.what());
+    return 2;
+  }
 }
 
 namespace {
@@ -1140,6 +1164,7 @@ bool bundle_gate_keep_h(const BundleH &b, const float dl[3], const float dh[3], 
 // [6] child slots tested, [7] deepest work stack (nodes).  Oriented-box nodes are walked per lane in both.
 extern "C" int32_t bzr_debug_traverse_bundle(const void *patches, uint32_t n, uint32_t stride, const float *rays,
                                              uint32_t nr, float max_spread, uint64_t stats[12]) {
+  try {
   if ((!patches && n) || (!rays && nr) || !stats || stride % 4 || stride < 264) return 1;
   bzr_host::Bvh far = bzr_host::build_bvh(static_cast<const float *>(patches), n, stride / 4, bzr_host::kTierFar);
   bzr_host::Bvh near = bzr_host::build_bvh(static_cast<const float *>(patches), n, stride / 4, bzr_host::kTierNear);
@@ -1258,32 +1283,51 @@ extern "C" int32_t bzr_debug_traverse_bundle(const void *patches, uint32_t n, ui
     for (uint32_t x : lane_leaves) stats[5] += !std::binary_search(bundle_leaves.begin(), bundle_leaves.end(), x);
   }
   return 0;
+  } catch (std::exception const &e) {  // build_bvh's invariant checks: a status, not a throw across the C ABI
+    bzr_internal_set_error(e.what());
+    return 2;
+  }
 }
 
 // The always list of one tier (patches without a proven gate region, ascending): count, and the indices
 // when `out` is not null.
 extern "C" int32_t bzr_debug_always_list(const void *patches, uint32_t n, uint32_t stride, int32_t tier, uint32_t *out,
                                          uint32_t *count) {
+  try {
   if ((!patches && n) || !count || stride % 4 || stride < 264) return 1;
   if (tier != bzr_host::kTierFar && tier != bzr_host::kTierNear) return 1;
   bzr_host::Bvh bvh = bzr_host::build_bvh(static_cast<const float *>(patches), n, stride / 4, tier);
   *count = static_cast<uint32_t>(bvh.always.size());
   if (out) std::memcpy(out, bvh.always.data(), bvh.always.size() * sizeof(uint32_t));
   return 0;
+  } catch (std::exception const &e) {  // build_bvh's invariant checks: a status, not a throw across the C ABI
+    bzr_internal_set_error(e.what());
+    return 2;
+  }
 }
 
 // The always list's wedge pre-test words (bvh.hpp Bvh::always_wedge), 8 floats per always-listed patch.
 extern "C" int32_t bzr_debug_always_wedges(const void *patches, uint32_t n, uint32_t stride, int32_t tier, float *out) {
+  try {
   if ((!patches && n) || !out || stride % 4 || stride < 264) return 1;
   if (tier != bzr_host::kTierFar && tier != bzr_host::kTierNear) return 1;
   bzr_host::Bvh bvh = bzr_host::build_bvh(static_cast<const float *>(patches), n, stride / 4, tier);
   std::memcpy(out, bvh.always_wedge.data(), bvh.always_wedge.size() * sizeof(float));
   return 0;
+  } catch (std::exception const &e) {  // build_bvh's invariant checks: a status, not a throw across the C ABI
+    bzr_internal_set_error(e.what());
+    return 2;
+  }
 }
 
 extern "C" int32_t bzr_debug_bounding_sphere(const void *patches, uint32_t n, uint32_t stride, float out[4]) {
+  try {
   if ((!patches && n) || !out || stride % 4 || stride < 264) return 1;
   bzr_host::Bvh bvh = bzr_host::build_bvh(static_cast<const float *>(patches), n, stride / 4);
   for (int k = 0; k < 4; ++k) out[k] = bvh.sphere[k];
   return 0;
+  } catch (std::exception const &e) {  // build_bvh's invariant checks: a status, not a throw across the C ABI
+    bzr_internal_set_error(e.what());
+    return 2;
+  }
 }

@@ -6,7 +6,8 @@
 #   STEPS="pytest smoke bench ..." selects steps (default: pytest smoke bench prof)
 #   RUN=name       output directory gpurun_out/$RUN (default gpurun_out)
 #   BENCH_ARGS     bench.py flags of the bench / rehearse2 steps
-#   PYTEST_ARGS    extra pytest args (e.g. -k pattern, a test file) of the pytest step
+#   PYTEST_K       pytest -k expression of the pytest step (e.g. "tiled or dropin")
+#   PYTEST_ARGS    other extra pytest args of the pytest step
 #   PROF_TAG, PROF_BENCH, PROF_WORKLOAD   the prof step: scripts/prof_run.sh (kernel trace + PMC passes)
 #   AB_ARGS        the ab step: scripts/ab.py arguments
 R="$GRAFT_REPO_ROOT"
@@ -27,15 +28,20 @@ nproc > "$OUT/host.txt"; lscpu | grep -m1 "Model name" >> "$OUT/host.txt"
 for s in $STEPS; do
   case $s in
     pytest) step pytest_gpu 900 python -u -m pytest tests -x -v -m gpu -p no:cacheprovider --timeout 120 \
-              --timeout-method thread ${PYTEST_ARGS:-} ;;
+              --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} ${PYTEST_ARGS:-} ;;
     smoke)  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)  step bench 600 python bench.py ${BENCH_ARGS:-} ;;
     # 2 ranks on the box's one GPU, launched by bench.py itself (no torch.distributed.run): gloo, every rank
     # on device 0 (RCCL refuses two ranks on one device).  Exercises the launcher, the tile deal and the
     # per-frame gather; not a scaling measurement.
-    rehearse2) BZR_BENCH_BACKEND=gloo BZR_BENCH_DEVICE=0 step rehearse2 300 python bench.py --gpus 2 --steps 5 \
+    rehearse2) step rehearse2 300 env BZR_BENCH_BACKEND=gloo BZR_BENCH_DEVICE=0 python bench.py --gpus 2 --steps 5 \
               --warmup 2 --cpu-baseline off ${BENCH_ARGS:-} ;;
-    prof)   TAG=${PROF_TAG:-prof} BENCH=${PROF_BENCH:-} WORKLOAD=${PROF_WORKLOAD:-} step prof 1500 bash scripts/prof_run.sh ;;
+    prof)   step prof 1500 env TAG="${PROF_TAG:-prof}" BENCH="${PROF_BENCH:-}" WORKLOAD="${PROF_WORKLOAD:-}" \
+              bash scripts/prof_run.sh ;;
     ab)     step ab 900 python scripts/ab.py ${AB_ARGS:-} ;;
+    # the far-origin overflow count of the default and the bundle-walk builds
+    bundleprobe) step bundleprobe_base 300 python scripts/bundle_overflow_probe.py &&
+              step bundleprobe_bundle 300 env BZR_LIBRARY="$R/cuda-bezier-triangle-raytracer_amd/lib/tracebundle/libbzr.so" \
+                python scripts/bundle_overflow_probe.py ;;
   esac
 done

@@ -2,7 +2,7 @@
 """Full-frame oracle digests (test infrastructure): run the CPU oracle (oracle/bzr_oracle.c, the C
 restatement of reference/bezierMesh.cpp:206-227, bezierTriangle.cpp:123-195, bezierLens.cpp:4-34 and the
 chain driver reference/test.cpp:376-401) over whole benchmark frames and commit one SHA-256 per 64x64 tile
-(layout: tests/golden/tile_digest.py).  tests/test_gpu_digests.py traces the same frames through libbzr
+(layout: tests/golden/tile_digest.py).  tests/test_gpu_fullsize.py traces the same frames through libbzr
 and compares tile by tile, so the bench configs' full-size output is pinned to the oracle bit for bit.
 
   d_cfg4_4096.npz   cfg4 (BASELINE configs[3], the bench workload): two lenses, refraction chain, the

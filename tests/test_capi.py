@@ -138,3 +138,24 @@ def test_pack_frame_validates_before_touching_a_device(bzr):
     for args, msg in cases:
         assert L.bzr_pack_frame(None, *args) == 1, args
         assert msg in L.bzr_last_error(), (args, L.bzr_last_error())
+
+
+def test_pack_frame_python_checks_buffer_sizes(bzr):
+    """bzr_amd.pack_frame checks the gather buffer against the layout's size and the rays' shape before the
+    device would write past it."""
+    torch = pytest.importorskip("torch")
+    n, npad, cap = 100, 4096, 64
+    st, sg = torch.zeros(n, dtype=torch.int32), torch.zeros(n, dtype=torch.int32)
+    rays = torch.zeros((6, n))
+    cases = [("rays", rays, torch.zeros(7 * npad - 1), "needs"),
+             ("image", None, torch.zeros(npad - 1), "needs"),
+             ("compact", rays, torch.zeros(npad // 4 + 1 + 6 * cap), "needs"),
+             ("rays", torch.zeros((7, n)), torch.zeros(7 * npad), r"\[6, 100\]"),
+             ("image", None, torch.zeros(npad), None)]
+    for layout, r, packed, msg in cases:
+        if msg is None:  # sizes fine: the call gets as far as the residency check (host tensors)
+            with pytest.raises(bzr.BzrError, match="device tensors"):
+                bzr.pack_frame(None, layout, r, st, sg, packed, npad, cap)
+        else:
+            with pytest.raises(bzr.BzrError, match=msg):
+                bzr.pack_frame(None, layout, r, st, sg, packed, npad, cap)

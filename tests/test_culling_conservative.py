@@ -266,6 +266,41 @@ def always_list(bzr, patches, tier):
     return out
 
 
+# A small lens with one rounding-dominated patch and no non-finite record: ellipsoid(16, 8, (1, 2, 2)) moved
+# so that patch 0's plane passes within 3e-6 of the origin (its always-hit box used to make the
+# illumination sphere infinite).
+DOMINATED_LENS_SHIFT = (3.099341, -0.02972891, -0.16860084)
+
+
+def dominated_lens(bzr):
+    m = bzr.TriMesh().make_ellipsoid(16, 8, (1.0, 2.0, 2.0))
+    m.translate(DOMINATED_LENS_SHIFT)
+    return m.standardize().bezier_patches()
+
+
+def test_bounding_sphere_survives_an_always_listed_patch(bzr):
+    """The illumination sphere is built over the proven (tree) boxes only: a lens with a rounding-dominated
+    patch keeps a finite sphere holding every proven box (bzr_illuminate tests the always list per ray)."""
+    patches = dominated_lens(bzr)
+    alw = always_list(bzr, patches, 0)
+    assert len(alw) == 1 and np.isfinite(patches[:, 49:58]).all()
+    boxes, _ = gate_boxes(bzr, patches)
+    L = bzr.lib()
+    fn = L.bzr_debug_bounding_sphere
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]
+    fn.restype = ctypes.c_int32
+    sph = np.zeros(4, np.float32)
+    p = np.ascontiguousarray(patches, np.float32)
+    assert fn(p.ctypes.data, len(p), 264, sph.ctypes.data) == 0
+    assert np.isfinite(sph).all()
+    keep = np.ones(len(p), bool)
+    keep[alw] = False
+    lo, hi = boxes[keep, :3].astype(np.float64), boxes[keep, 3:].astype(np.float64)
+    corners = np.stack([np.where([(c >> a) & 1 for a in range(3)], hi, lo) for c in range(8)])
+    assert np.linalg.norm(corners - sph[:3].astype(np.float64), axis=2).max() <= float(sph[3])
+    assert float(sph[3]) < 10.0
+
+
 @pytest.mark.parametrize("cfg_name,expect", [("cfg1", 0), ("cfg2", 0), ("cfg3", 0), ("cfg5", 126)])
 def test_rounding_dominated_patches_are_always_tested(bzr, cfg_name, expect):
     """Culling is exact by construction: a patch is in the tree only if its gate region is proven

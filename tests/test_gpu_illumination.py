@@ -96,6 +96,33 @@ def test_illuminate_matches_oracle(bzr, orc, ctx, cfg_name, n, x):
     assert (status[culled] == 0).all() and (seg[culled] == 1).all()
 
 
+def test_illuminate_with_an_always_listed_patch(bzr, orc, ctx):
+    """A lens with a rounding-dominated patch (no proven gate region: always listed): the sphere covers the
+    proven boxes only, and a ray outside it is culled only if no always-listed gate passes -- the counts
+    still equal the oracle's uncut chain, and the cull still drops most of an emitter far behind the lens."""
+    from test_culling_conservative import dominated_lens
+
+    lens = dominated_lens(bzr)
+    dm = bzr.DeviceMesh(ctx, lens)
+    sph = bzr.bounding_sphere(dm)
+    assert np.isfinite(sph).all()
+    n = 1 << 15
+    for x in (0.0, -60.0):
+        hist, stats = bzr.illuminate(ctx, [dm], [1.3], emitter(bzr, x=x), n, target(bzr))
+        rays, status, seg, want_hist, exited, landed = oracle_illuminate(orc, [lens], [1.3], emitter(orc, x=x), n,
+                                                                         target(orc))
+        assert stats["exited"] == exited and stats["landed"] == landed
+        assert np.array_equal(hist, want_hist)
+        c = sph.astype(np.float64)
+        oc = rays[:3].astype(np.float64) - c[:3, None]
+        cc = (oc * oc).sum(0) - c[3] ** 2
+        b = (oc * rays[3:].astype(np.float64)).sum(0)
+        outside = (cc > 0) & ((b >= 0) | (b * b - cc < 0))
+        assert stats["culled"] <= outside.sum()
+        if x == -60.0:
+            assert stats["culled"] > n // 2
+
+
 @pytest.mark.slow
 def test_illuminate_two_batches(bzr, orc, ctx):
     """More rays than one 1M-ray batch: the batches continue the global ray numbering."""
