@@ -182,6 +182,12 @@ constexpr int kTravBlock = BZR_TRAV_BLOCK;
 #define BZR_NEWTON_GATED 1
 #endif
 // A 64-pair chunk with more distinct patches than this goes to k_newton_lane (one record per lane).
+// BZR_STAGED_AOS (default 0): k_traverse also writes each ray of the chunk as a 32-byte AoS record (ox oy oz dx
+// | dy dz), and the Newton / resolve kernels read a pair's ray from it -- one 32-byte sector instead of six
+// SoA rows whose 128-byte lines serve few of a bucket's rays.
+#ifndef BZR_STAGED_AOS
+#define BZR_STAGED_AOS 0
+#endif
 #ifndef BZR_LANE_THRESHOLD
 #define BZR_LANE_THRESHOLD 3
 #endif
@@ -334,6 +340,21 @@ __device__ __forceinline__ void load_ray(const float *__restrict__ r, uint32_t n
   s = mk(r[i], r[(size_t)n + i], r[(size_t)2 * n + i]);
   d = mk(r[(size_t)3 * n + i], r[(size_t)4 * n + i], r[(size_t)5 * n + i]);
 }
+// A pair's ray in the staged path: the chunk's 32-byte AoS copy (BZR_STAGED_AOS) or the SoA rows.
+__device__ __forceinline__ void load_pair_ray(const float4 *__restrict__ aos, const float *__restrict__ r, uint32_t ld,
+                                              uint32_t off, uint32_t i, f3 &s, f3 &d) {
+#if BZR_STAGED_AOS
+  (void)r;
+  (void)ld;
+  (void)off;
+  const float4 a = aos[2u * i], b = aos[2u * i + 1u];
+  s = mk(a.x, a.y, a.z);
+  d = mk(a.w, b.x, b.y);
+#else
+  (void)aos;
+  load_ray(r, ld, off + i, s, d);
+#endif
+}
 __device__ __forceinline__ void store_ray(float *__restrict__ r, uint32_t n, uint32_t i, f3 s, f3 d) {
   r[i] = s.x;
   r[(size_t)n + i] = s.y;
@@ -471,6 +492,7 @@ struct Work {
   uint32_t *fol;     // [cap] pair | what << 30
   uint32_t *ovf;     // [n]
   uint32_t *lanes;   // [cap / 64 + 1] chunks for k_newton_lane (count in ctr[3])
+  float4 *aos;       // [2 * chunk] the chunk's rays as 32-byte records (BZR_STAGED_AOS)
   void *cub;
   size_t cub_bytes;
   uint32_t cap;      // kMaxCand * chunk
@@ -873,6 +895,12 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
   bool active = i < n && (alive == nullptr || alive[off + i] != BZR_RR_NONE);
   f3 s = mk(0.0f, 0.0f, 0.0f), d = s;
   if (i < n) load_ray(rays, ld, off + i, s, d);
+#if BZR_STAGED_AOS
+  if (i < n) {
+    w.aos[2u * i] = make_float4(s.x, s.y, s.z, d.x);
+    w.aos[2u * i + 1u] = make_float4(d.y, d.z, 0.0f, 0.0f);
+  }
+#endif
   uint32_t cnt = 0;
   // gate-region boxes hold for ray origins within s_max (bvh.cpp); farther rays take the full scan
   if (active && !(fmaxf(fmaxf(fabsf(s.x), fabsf(s.y)), fabsf(s.z)) <= m.s_max)) {
@@ -1196,7 +1224,8 @@ __global__ __launch_bounds__(kBlock) BZR_NEWTON_ATTR void k_newton(const float *
                                                    uint32_t ld, uint32_t off, float *__restrict__ slot,
                                                    uint32_t cap, unsigned long long *__restrict__ key,
                                                    uint32_t *__restrict__ fol, uint32_t *__restrict__ nfol,
-                                                   uint32_t *__restrict__ lanes, uint32_t *__restrict__ nlanes) {
+                                                   uint32_t *__restrict__ lanes, uint32_t *__restrict__ nlanes,
+                                                   const float4 *__restrict__ aos) {
   __shared__ uint32_t fbuf[kWaves][kFolBuf];
   const uint32_t wv = threadIdx.x >> 6;
   uint32_t nf = 0;  // staged follow requests of this wave (uniform)
@@ -1216,7 +1245,7 @@ __global__ __launch_bounds__(kBlock) BZR_NEWTON_ATTR void k_newton(const float *
     bool todo = p < P;
     const uint32_t ray = pr.x, b = pr.y;
     f3 s = mk(0.0f, 0.0f, 0.0f), d = s;
-    if (todo) load_ray(rays, ld, off + ray, s, d);  // pairs of one patch: mostly neighbouring rays
+    if (todo) load_pair_ray(aos, rays, ld, off, ray, s, d);  // pairs of one patch: mostly neighbouring rays
     const uint32_t qn = q + W, pn = qn * 64u + lane;  // prefetch the next chunk's pair records
     if (qn < nchunks && pn < P) pr = pairs[pn];
     bool is_fol = false;
@@ -1264,7 +1293,8 @@ __global__ __launch_bounds__(kBlock) void k_newton_lane(const float *__restrict_
                                                         uint32_t cap, unsigned long long *__restrict__ key,
                                                         uint32_t *__restrict__ fol, uint32_t *__restrict__ nfol,
                                                         const uint32_t *__restrict__ lanes,
-                                                        const uint32_t *__restrict__ nlanes) {
+                                                        const uint32_t *__restrict__ nlanes,
+                                                        const float4 *__restrict__ aos) {
   const uint32_t P = __builtin_amdgcn_readfirstlane(*total);
   const uint32_t C = __builtin_amdgcn_readfirstlane(*nlanes);
   const uint32_t lane = threadIdx.x & 63u;
@@ -1276,7 +1306,7 @@ __global__ __launch_bounds__(kBlock) void k_newton_lane(const float *__restrict_
       const uint2 pr = pairs[p];
       const uint32_t b = pr.y;
       f3 s, d;
-      load_ray(rays, ld, off + pr.x, s, d);
+      load_pair_ray(aos, rays, ld, off, pr.x, s, d);
       const Patch pa = load_patch(full + (size_t)rec::kWords * b);
       const Hit h = patch_intersect<BZR_NEWTON_GATED != 0, kFast>(pa, s, d, false);
       if (h.what == kIntersect) record(slot, cap, p, h, b, &key[pr.x]);
@@ -1353,7 +1383,7 @@ __global__ __launch_bounds__(kBlock) void k_resolve(MeshView m, const float *__r
     const uint32_t f = w.fol[q], p = f & 0x3FFFFFFFu, what = f >> 30;
     const uint2 pr = w.pairs[p];
     f3 s, d;
-    load_ray(rays, ld, off + pr.x, s, d);
+    load_pair_ray(w.aos, rays, ld, off, pr.x, s, d);
     const uint32_t nbr = __float_as_uint(m.full[(size_t)rec::kWords * pr.y + rec::kNeigh + what]);
     Patch pa = load_patch(m.full + (size_t)rec::kWords * nbr);
     Hit h = patch_intersect<false, kFast>(pa, s, d, true);
@@ -1366,7 +1396,7 @@ __global__ __launch_bounds__(kBlock) void k_resolve(MeshView m, const float *__r
     const uint32_t q = (uint32_t)(item / S), lo = (uint32_t)(item - (uint64_t)q * S) * kOvfSlice, hi = min(m.n, lo + kOvfSlice);
     const uint32_t i = w.ovf[q];
     f3 s, d;
-    load_ray(rays, ld, off + i, s, d);
+    load_pair_ray(w.aos, rays, ld, off, i, s, d);
     float best_t = FLT_MAX;
     uint32_t best_b = 0xFFFFFFFFu;
 #pragma unroll 4
@@ -2030,6 +2060,15 @@ __global__ __launch_bounds__(kTraceBlock) BZR_TRACE_ATTR void k_trace(LensSet le
   }
 }
 
+// BZR_TRACE_RPL (default 1): rays per lane of the fused kernel.  2 or 4: k_trace_r (trace_pool.inc), one wave
+// per 64 R rays with the Newton passes pooled over all of them.
+#ifndef BZR_TRACE_RPL
+#define BZR_TRACE_RPL 1
+#endif
+#if BZR_TRACE_RPL > 1
+#include "trace_pool.inc"
+#endif
+
 // ------------------------------------------------------------ brute-force path
 __global__ __launch_bounds__(kBlock) void k_intersect_scan(MeshView m, const float *__restrict__ rays, uint32_t n,
                                                            float *__restrict__ hits) {
@@ -2260,7 +2299,7 @@ bzr_status ensure_work(bzr_ctx *ctx, uint32_t chunk, uint32_t nb, Work &w) {
   const size_t bytes = round256(32) + round256((size_t)(hn + 1) * 4) + round256((size_t)(hn + 1) * 4) + 2 * round256(cap * 4) +
                        round256((size_t)chunk * 4) + round256((size_t)chunk * 8) + round256(kSlotWords * cap * 4) +
                        round256(cap * 8) + round256(cap * 4) + round256((size_t)chunk * 4) + round256((cap / 64 + 1) * 4) +
-                       round256(cub_bytes);
+                       (BZR_STAGED_AOS ? round256((size_t)chunk * 32) : 0) + round256(cub_bytes);
   const size_t had = ctx->work_bytes;
   if (bzr_status s = ensure_buffer(ctx->work, ctx->work_bytes, bytes)) return s;
   if (ctx->work_bytes != had) ctx->zero_ctr = nullptr;  // reallocated (possibly at the same address)
@@ -2277,6 +2316,7 @@ bzr_status ensure_work(bzr_ctx *ctx, uint32_t chunk, uint32_t nb, Work &w) {
   w.fol = st.take<uint32_t>(cap);
   w.ovf = st.take<uint32_t>(chunk);
   w.lanes = st.take<uint32_t>(cap / 64 + 1);
+  w.aos = BZR_STAGED_AOS ? st.take<float4>((size_t)2 * chunk) : nullptr;
   w.cub = st.take<char>(cub_bytes ? cub_bytes : 1);
   w.cub_bytes = cub_bytes;
   w.cap = static_cast<uint32_t>(cap);
@@ -2292,7 +2332,7 @@ bzr_status ensure_work(bzr_ctx *ctx, uint32_t chunk, uint32_t nb, Work &w) {
 #define BZR_CHUNK_LOG2 23
 #endif
 constexpr uint32_t kChunk = 1u << BZR_CHUNK_LOG2;
-constexpr size_t kWorkBytesPerRay = (size_t)kMaxCand * (4 + 4 + 48 + 8 + 4) + 16;
+constexpr size_t kWorkBytesPerRay = (size_t)kMaxCand * (4 + 4 + 48 + 8 + 4) + 16 + (BZR_STAGED_AOS ? 32 : 0);
 uint32_t chunk_for(bzr_ctx *ctx, uint64_t n) {
   if (!ctx->chunk_cap) {
     size_t free_b = 0, total_b = 0;
@@ -2331,9 +2371,10 @@ bzr_status run_culled(bzr_ctx *ctx, const MeshView &mv, const float *rays, uint3
   const uint32_t gn = std::min<uint32_t>(std::max<uint32_t>((kMaxCand * n + kBlock - 1) / kBlock, 1u),
                                          resident_blocks(ctx, k_newton<kFast>));
   launch(ctx, BZR_KERNEL_NEWTON, k_newton<kFast>, dim3(gn), mv.full, w.offs + hn, w.pairs, rays, ld, off, w.slot, w.cap, w.key, w.fol,
-         w.ctr, w.lanes, w.ctr + 3);
+         w.ctr, w.lanes, w.ctr + 3, (const float4 *)w.aos);
   launch(ctx, BZR_KERNEL_NEWTON_LANE, k_newton_lane<kFast>, dim3(std::min<uint32_t>(std::max<uint32_t>(n / 1024u, 1u), 1024u)),
-         mv.full, w.offs + hn, w.pairs, rays, ld, off, w.slot, w.cap, w.key, w.fol, w.ctr, w.lanes, w.ctr + 3);
+         mv.full, w.offs + hn, w.pairs, rays, ld, off, w.slot, w.cap, w.key, w.fol, w.ctr, w.lanes, w.ctr + 3,
+         (const float4 *)w.aos);
   {  // follow retries + overflow rays (whose keys the Newton stage left untouched: their lists are empty)
     const uint64_t items = (uint64_t)n * ((nb + kOvfSlice - 1) / kOvfSlice);
     const uint32_t grid = std::max(std::min<uint32_t>(grid_for(n / 8 + 1), 1024u),
@@ -2360,6 +2401,20 @@ bzr_status run_fused(bzr_ctx *ctx, const LensSet &set, const TraceJob &job, uint
   TraceJob j = job;
   j.wave_clock = (ctx->wave_clock && ctx->wave_clock_cap >= (job.n + 63) / 64) ? ctx->wave_clock : nullptr;
   j.wave_real = ctx->wave_clock_real ? 1u : 0u;
+#if BZR_TRACE_RPL > 1
+  constexpr uint32_t kRays = 64u * BZR_TRACE_RPL;  // rays per one-wave block (k_trace_r)
+  const dim3 rgrid((job.n + kRays - 1) / kRays), rblock(64);
+  auto go = [&](auto kernel) { launch_on(ctx, ctx->stream, rblock, BZR_KERNEL_TRACE, kernel, rgrid, set, j, ctx->counters); };
+  (void)grid;
+  (void)block;
+  if (fast) {
+    if (count) go(k_trace_r<kMode, BZR_TRACE_RPL, true, true>);
+    else go(k_trace_r<kMode, BZR_TRACE_RPL, true, false>);
+  } else {
+    if (count) go(k_trace_r<kMode, BZR_TRACE_RPL, false, true>);
+    else go(k_trace_r<kMode, BZR_TRACE_RPL, false, false>);
+  }
+#else
   auto go = [&](auto kernel) { launch_on(ctx, ctx->stream, block, BZR_KERNEL_TRACE, kernel, grid, set, j, ctx->counters); };
   if (fast) {
     if (count) go(k_trace<kMode, true, true>);
@@ -2368,6 +2423,7 @@ bzr_status run_fused(bzr_ctx *ctx, const LensSet &set, const TraceJob &job, uint
     if (count) go(k_trace<kMode, false, true>);
     else go(k_trace<kMode, false, false>);
   }
+#endif
   BZR_HIP(hipGetLastError());
   return BZR_OK;
 }

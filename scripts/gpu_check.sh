@@ -9,7 +9,7 @@
 #   PYTEST_K       pytest -k expression of the pytest step (e.g. "tiled or dropin")
 #   PYTEST_ARGS    other extra pytest args of the pytest step
 #   PROF_TAG, PROF_BENCH, PROF_WORKLOAD   the prof step: scripts/prof_run.sh (kernel trace + PMC passes)
-#   AB_ARGS        the ab step: scripts/ab.py arguments
+#   AB_ARGS, AB2_ARGS, AB3_ARGS   the ab / ab2 / ab3 steps: scripts/ab.py arguments
 R="$GRAFT_REPO_ROOT"
 cd "$R" || exit 2
 OUT="$R/gpurun_out/${RUN:-.}"
@@ -39,6 +39,8 @@ for s in $STEPS; do
     prof)   step prof 1500 env TAG="${PROF_TAG:-prof}" BENCH="${PROF_BENCH:-}" WORKLOAD="${PROF_WORKLOAD:-}" \
               bash scripts/prof_run.sh ;;
     ab)     step ab 900 python scripts/ab.py ${AB_ARGS:-} ;;
+    ab2)    step ab2 900 python scripts/ab.py ${AB2_ARGS:-} ;;
+    ab3)    step ab3 900 python scripts/ab.py ${AB3_ARGS:-} ;;
     # the far-origin overflow count of the default and the bundle-walk builds
     bundleprobe) step bundleprobe_base 300 python scripts/bundle_overflow_probe.py &&
               step bundleprobe_bundle 300 env BZR_LIBRARY="$R/cuda-bezier-triangle-raytracer_amd/lib/tracebundle/libbzr.so" \

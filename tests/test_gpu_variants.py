@@ -7,6 +7,10 @@ joined retry state must stay valid across the switch.  The default 64-entry stac
 bench configs, so only this build exercises that path: fused == staged == brute force (and == the oracle
 on cfg2), bit for bit, with the device counters reporting overflow rays.
 
+rpl2 / rpl4: libbzr whose fused kernel is k_trace_r (trace_pool.inc): 2 or 4 rays per lane, the Newton passes
+pooled over a wave's 128 / 256 rays (-DBZR_TRACE_RPL); the same checks plus cfg4's two-lens chain and origins
+beyond s_max (the in-order scan inside the pooled kernel), fused == brute force == the oracle.
+
 tracebundle: libbzr with k_trace's wave-bundle walk (-DBZR_TRACE_BUNDLE=1, off by default; k_traverse uses
 it by default): the same checks, fused == staged == brute force (== the oracle on cfg2), including the
 incoherent cfg5 rays whose wide bundles take the per-lane node tests.
@@ -69,6 +73,32 @@ for name, mode in (("fused", bzr.PIPELINE_FUSED), ("staged", bzr.PIPELINE_STAGED
     cnt = ctx.counters_report(); ctx.counters(False)
     out[f"cfg5_{name}_equal"] = bool(np.array_equal(got, ref))
     out[f"cfg5_{name}_overflow_rays"] = cnt["overflow_rays"]
+if "--more" in sys.argv:
+    # cfg4: two lenses, the chain, 256^2 primaries: fused == brute force == the oracle
+    l4 = [build_lens(bzr.TriMesh, l).bezier_patches() for l in CONFIGS["cfg4"].lenses]
+    d4 = [bzr.DeviceMesh(ctx, p) for p in l4]
+    r4 = grid_rays(CONFIGS["cfg4"], side=256)
+    w4 = orc.trace_chain(l4, [1.3, 1.3], r4)
+    for name, mode in (("fused", bzr.PIPELINE_FUSED), ("brute", bzr.ACCEL_NONE)):
+        g4 = bzr.trace_chain(ctx, d4, [1.3, 1.3], r4, mode=mode)
+        out[f"cfg4_{name}_equal"] = all(np.array_equal(bits(g), bits(w)) for g, w in zip(g4, w4))
+    # origins beyond s_max mixed into the waves (the in-order scan): robot.stl, 25 % far
+    lr = build_lens(bzr.TriMesh, CONFIGS["cfg3"].lenses[0].__class__("stl", split=1)).bezier_patches()
+    dr = bzr.DeviceMesh(ctx, lr)
+    rng = np.random.default_rng(11)
+    o = rng.uniform(-30, 30, (3, 4096)).astype(np.float32)
+    far = rng.random(4096) < 0.25
+    o[0, far] = np.float32(-5e4)
+    t = rng.uniform(-20, 20, (3, 4096)).astype(np.float32)
+    dd = t - o
+    dd /= np.sqrt((dd * dd).sum(axis=0, keepdims=True)).astype(np.float32)
+    rr = np.concatenate([o, dd.astype(np.float32)]).astype(np.float32)
+    ctx.counters(True); ctx.counters_report()
+    gf = bits(bzr.intersect(ctx, dr, rr, mode=bzr.PIPELINE_FUSED))
+    cnt = ctx.counters_report(); ctx.counters(False)
+    out["far_fused_equal"] = bool(np.array_equal(gf, bits(orc.intersect(lr, rr))))
+    out["far_overflow_rays"] = cnt["overflow_rays"]
+    out["far_count"] = int(far.sum())
 print(json.dumps(out))
 """
 
@@ -106,3 +136,23 @@ def test_trace_bundle_walk_is_exact():
         if k.endswith("_equal"):
             assert v, (k, out)
     assert out["cfg5_hits"] > 10000
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", ["rpl2", "rpl4"])
+def test_pooled_passes_are_exact(variant):
+    """k_trace_r (2 / 4 rays per lane, Newton passes pooled over the wave's rays): bit-identical to the
+    brute-force scan and the oracle on cfg2 / cfg4 chains, cfg5 intersect and far origins."""
+    lib = PKG / "lib" / variant / "libbzr.so"
+    if not lib.exists():
+        pytest.fail(f"{lib} missing: build() makes the `variants` target")
+    env = dict(os.environ, BZR_LIBRARY=str(lib))
+    res = subprocess.run([sys.executable, "-c", WORKER, str(PKG), str(REPO), "--more"], env=env,
+                         capture_output=True, text=True, timeout=110)
+    assert res.returncode == 0, res.stderr[-2000:]
+    out = json.loads(res.stdout.strip().splitlines()[-1])
+    for k, v in out.items():
+        if k.endswith("_equal"):
+            assert v, (k, out)
+    assert out["cfg2_fused_overflow_rays"] == 0 and out["cfg5_fused_overflow_rays"] == 0
+    assert out["far_overflow_rays"] == out["far_count"]
