@@ -38,6 +38,7 @@ for s in $STEPS; do
               --warmup 2 --cpu-baseline off ${BENCH_ARGS:-} ;;
     prof)   step prof 1500 env TAG="${PROF_TAG:-prof}" BENCH="${PROF_BENCH:-}" WORKLOAD="${PROF_WORKLOAD:-}" \
               bash scripts/prof_run.sh ;;
+    dropin) step dropin 400 bash scripts/dropin_latency.sh ;;
     ab)     step ab 900 python scripts/ab.py ${AB_ARGS:-} ;;
     ab2)    step ab2 900 python scripts/ab.py ${AB2_ARGS:-} ;;
     ab3)    step ab3 900 python scripts/ab.py ${AB3_ARGS:-} ;;

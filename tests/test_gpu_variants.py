@@ -124,17 +124,22 @@ def test_tiny_stack_overflow_path_is_exact():
 
 @pytest.mark.gpu
 def test_trace_bundle_walk_is_exact():
+    """The wave-bundle walk in k_trace: exact, and only the far origins take the in-order scan (round 3's
+    4096-of-1026 count came from a pre-release bundle walk whose full-stack batches sent whole incoherent
+    waves to the scan; the released one tests wide bundles per lane -- profiles/r04_bundle_overflow_probe.jsonl)."""
     lib = PKG / "lib" / "tracebundle" / "libbzr.so"
     if not lib.exists():
         pytest.fail(f"{lib} missing: build() makes the `variants` target")
     env = dict(os.environ, BZR_LIBRARY=str(lib))
-    res = subprocess.run([sys.executable, "-c", WORKER, str(PKG), str(REPO)], env=env, capture_output=True,
+    res = subprocess.run([sys.executable, "-c", WORKER, str(PKG), str(REPO), "--more"], env=env, capture_output=True,
                          text=True, timeout=110)
     assert res.returncode == 0, res.stderr[-2000:]
     out = json.loads(res.stdout.strip().splitlines()[-1])
     for k, v in out.items():
         if k.endswith("_equal"):
             assert v, (k, out)
+    assert out["far_overflow_rays"] == out["far_count"]
+    assert out["cfg2_fused_overflow_rays"] == 0
     assert out["cfg5_hits"] > 10000
 
 
