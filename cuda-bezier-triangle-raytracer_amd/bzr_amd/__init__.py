@@ -83,6 +83,8 @@ _SIGS = {
     "bzr_tiled_trace": [_P, _P, _P, _U32, _P, _P, _P, _U32],
     "bzr_tiled_stream": [_P, ctypes.POINTER(_P)],
     "bzr_tiled_sync": [_P],
+    "bzr_tiled_set_layout": [_P, _I32, _U32],
+    "bzr_tiled_calibrate": [_P, _P, _P, _U32, _U32, ctypes.POINTER(_U32)],
     "bzr_mesh_interpolate": [_P, _P, _I32, _P, _U32],
     "bzr_emit": [_P, _P, ctypes.c_uint64, _U32, _P, _P, _U32],
     "bzr_illuminate": [_P, _P, _P, _U32, _P, ctypes.c_uint64, _P, _P, _P, _U32],
@@ -485,6 +487,20 @@ class TiledPlan:
 
     def sync(self):
         _check(lib().bzr_tiled_sync(self.handle))
+
+    def set_layout(self, layout: str, cap: int = 0):
+        """"rays" (28 B per ray) or "compact" (survivors only, up to `cap` per device share)."""
+        _check(lib().bzr_tiled_set_layout(self.handle, PACK_LAYOUTS[layout], cap))
+
+    def calibrate(self, lenses, ri, mode=MODE_PARITY) -> int:
+        """One synchronous frame, then the compact layout sized from its survivors; returns the capacity."""
+        nl = len(ri)
+        hs = (_P * (self.ndev * nl))(*[m.handle for ls in lenses for m in ls])
+        ris = (_F * nl)(*[float(x) for x in ri])
+        cap = _U32(0)
+        _check(lib().bzr_tiled_calibrate(self.handle, ctypes.cast(hs, _P), ctypes.cast(ris, _P), nl, mode,
+                                          ctypes.byref(cap)))
+        return int(cap.value)
 
     def close(self):
         if getattr(self, "handle", None):

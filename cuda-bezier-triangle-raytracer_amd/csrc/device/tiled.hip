@@ -4,12 +4,16 @@
 // A plan (bzr_tiled) deals the tiles of a tile-major frame round-robin to ndev devices: device d owns tiles
 // d, d + ndev, d + 2 ndev, ... packed back to back (its "share").  Per frame, on slot s = frame % nslot:
 //   1. device d traces its share on ctxs[s * ndev + d]'s stream (bzr_trace_chain, device pointers);
-//   2. packs it in bzr_pack_frame's rays layout, [7][npad] floats (6 ray rows + status | segments << 8);
+//   2. packs it in bzr_pack_frame's rays layout, [7][npad] floats (6 ray rows + status | segments << 8), or
+//      (bzr_tiled_set_layout / bzr_tiled_calibrate) its compact layout: a status/segment byte per ray, the
+//      survivor count and the final rays of the survivors only, up to a capacity per share;
 //   3. the packed shares travel to device 0: RCCL (ncclCommInitAll over the devices, one grouped call of
 //      ncclSend from every rank to rank 0 and ncclRecv of every rank on rank 0 -- rank 0 included, so a
 //      one-device plan runs the same collective code) on a plan-owned stream per device, or hipMemcpyPeerAsync
 //      when two list entries are the same device (RCCL needs distinct devices);
-//   4. k_tiled_unpack on device 0 scatters the gathered shares into the caller's outputs in input order.
+//   4. k_tiled_unpack on device 0 scatters the gathered shares into the caller's outputs in input order
+//      (compact: three kernels -- survivor counts per 1024 columns, their scan per share with the capacity
+//      check, the scatter; a ray that never refracted gets its primary ray back from device 0's copy).
 // Events order the steps without host waits: the gather waits for each device's pack, the next frame on the
 // same slot packs only after that slot's previous gather has left the buffer, device 0's stream of the
 // gather serialises the receive buffers.  Bytes: 28 per primary cross to device 0, (ndev - 1) / ndev of them
@@ -66,19 +70,144 @@ __global__ __launch_bounds__(kThreads) void k_share_extract(const float *__restr
 }
 
 // Device 0: the gathered shares recv[d][7][npad] -> frame-ordered outputs.
-__global__ __launch_bounds__(kThreads) void k_tiled_unpack(const float *__restrict__ recv, uint32_t ndev, uint32_t npad,
-                                                           uint32_t tile_rays, uint32_t n, float *__restrict__ out_rays,
-                                                           uint32_t *__restrict__ out_status,
+__global__ __launch_bounds__(kThreads) void k_tiled_unpack(const float *__restrict__ recv, size_t stride, uint32_t ndev,
+                                                           uint32_t npad, uint32_t tile_rays, uint32_t n,
+                                                           float *__restrict__ out_rays, uint32_t *__restrict__ out_status,
                                                            uint32_t *__restrict__ out_segments) {
   const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
   if (i >= n) return;
   const uint32_t k = i / tile_rays, d = k % ndev, col = (k / ndev) * tile_rays + (i - k * tile_rays);
-  const float *p = recv + (size_t)d * kRows * npad + col;
+  const float *p = recv + (size_t)d * stride + col;
 #pragma unroll
   for (uint32_t r = 0; r < 6u; ++r) out_rays[(size_t)r * n + i] = p[(size_t)r * npad];
   const uint32_t word = __float_as_uint(p[(size_t)6 * npad]);
   out_status[i] = word & 0xFFu;
   if (out_segments) out_segments[i] = word >> 8;
+}
+
+// Calibration (device 0): survivors of a traced frame per share (frame order in, the deal's share index out).
+__global__ __launch_bounds__(kThreads) void k_count_survivors(const uint32_t *__restrict__ status,
+                                                              const uint32_t *__restrict__ segments, uint32_t n,
+                                                              uint32_t ndev, uint32_t tile_rays,
+                                                              uint32_t *__restrict__ count) {
+  const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
+  if (i >= n) return;
+  if (segments[i] >= 2u || status[i] != 0u) atomicAdd(&count[(i / tile_rays) % ndev], 1u);
+}
+
+constexpr uint32_t kUnpackThreads = 256;
+constexpr uint32_t kUnpackCols = 4 * kUnpackThreads;  // columns per block (bzr_pack_frame's compact blocks)
+constexpr uint32_t kUnpackScan = 1024;
+
+__device__ __forceinline__ bool survivor_byte(uint32_t b) { return (b >> 2) >= 2u || (b & 3u) != 0u; }
+
+// Compact pass 1 (device 0): survivors among the columns of block b of share d (blockIdx = d * nblk + b).
+__global__ __launch_bounds__(kUnpackThreads) void k_unpack_count(const float *__restrict__ recv, size_t stride,
+                                                                 const uint32_t *__restrict__ share, uint32_t nblk,
+                                                                 uint32_t *__restrict__ block_count) {
+  __shared__ uint32_t wave_sum[kUnpackThreads / 64];
+  const uint32_t d = blockIdx.x / nblk, b = blockIdx.x - d * nblk, nd = share[d];
+  const unsigned char *bytes = reinterpret_cast<const unsigned char *>(recv + (size_t)d * stride);
+  uint32_t mine = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < 4u; ++k) {
+    const uint32_t col = b * kUnpackCols + k * kUnpackThreads + threadIdx.x;
+    mine += (uint32_t)__popcll(__ballot(col < nd && survivor_byte(bytes[col])));
+  }
+  if ((threadIdx.x & 63u) == 0u) wave_sum[threadIdx.x >> 6] = mine;
+  __syncthreads();
+  if (threadIdx.x == 0u) {
+    uint32_t t = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < kUnpackThreads / 64; ++w) t += wave_sum[w];
+    block_count[blockIdx.x] = t;
+  }
+}
+
+// Compact pass 2 (device 0, one block per share): exclusive offsets of the block counts; a share whose
+// survivors do not match its count word, or exceed the capacity, raises the overflow flag (its frame was
+// not fully gathered).
+__global__ __launch_bounds__(kUnpackScan) void k_unpack_scan(const float *__restrict__ recv, size_t stride, uint32_t cpad,
+                                                             uint32_t cap, const uint32_t *__restrict__ share, uint32_t nblk,
+                                                             const uint32_t *__restrict__ block_count,
+                                                             uint32_t *__restrict__ block_off, uint32_t *__restrict__ flag) {
+  __shared__ uint32_t part[kUnpackScan];
+  const uint32_t d = blockIdx.x;
+  const uint32_t *bc = block_count + (size_t)d * nblk;
+  uint32_t *bo = block_off + (size_t)d * nblk;
+  const uint32_t per = (nblk + kUnpackScan - 1) / kUnpackScan;
+  const uint32_t lo = threadIdx.x * per, hi = min(nblk, lo + per);
+  uint32_t sum = 0;
+  for (uint32_t b = lo; b < hi; ++b) sum += bc[b];
+  part[threadIdx.x] = sum;
+  __syncthreads();
+  for (uint32_t k = 1; k < kUnpackScan; k <<= 1) {
+    const uint32_t v = threadIdx.x >= k ? part[threadIdx.x - k] : 0u;
+    __syncthreads();
+    part[threadIdx.x] += v;
+    __syncthreads();
+  }
+  uint32_t run = threadIdx.x ? part[threadIdx.x - 1] : 0u;
+  for (uint32_t b = lo; b < hi; ++b) {
+    bo[b] = run;
+    run += bc[b];
+  }
+  if (threadIdx.x == kUnpackScan - 1 && share[d] > 0u) {  // (an empty share packed nothing)
+    const uint32_t total = part[kUnpackScan - 1];
+    const uint32_t count = __float_as_uint(recv[(size_t)d * stride + cpad / 4u]);
+    if (total != count || count > cap) atomicOr(flag, 1u);
+  }
+}
+
+// Compact pass 3 (device 0): every column of share d to its frame position -- a survivor's final ray from
+// the packed rows (its rank among the share's survivors), anyone else's primary ray from prim.
+__global__ __launch_bounds__(kUnpackThreads) void k_unpack_compact(const float *__restrict__ recv, size_t stride,
+                                                                   uint32_t cpad, uint32_t cap,
+                                                                   const uint32_t *__restrict__ share, uint32_t nblk,
+                                                                   const uint32_t *__restrict__ block_off,
+                                                                   const float *__restrict__ prim, uint32_t ndev,
+                                                                   uint32_t tile_rays, uint32_t n,
+                                                                   float *__restrict__ out_rays,
+                                                                   uint32_t *__restrict__ out_status,
+                                                                   uint32_t *__restrict__ out_segments) {
+  __shared__ uint32_t cnt[4][kUnpackThreads / 64];
+  const uint32_t d = blockIdx.x / nblk, b = blockIdx.x - d * nblk, nd = share[d];
+  const float *base = recv + (size_t)d * stride;
+  const unsigned char *bytes = reinterpret_cast<const unsigned char *>(base);
+  const float *rows = base + cpad / 4u + 1u;
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  bool keep[4];
+  uint32_t byte[4];
+  unsigned long long bal[4];
+#pragma unroll
+  for (uint32_t k = 0; k < 4u; ++k) {
+    const uint32_t col = b * kUnpackCols + k * kUnpackThreads + threadIdx.x;
+    byte[k] = col < nd ? bytes[col] : 0u;
+    keep[k] = col < nd && survivor_byte(byte[k]);
+    bal[k] = __ballot(keep[k]);
+    if (lane == 0u) cnt[k][w] = (uint32_t)__popcll(bal[k]);
+  }
+  __syncthreads();
+  const uint32_t off = block_off[(size_t)d * nblk + b];
+  const unsigned long long below = lane ? (~0ull >> (64u - lane)) : 0ull;
+  uint32_t before = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < 4u; ++k) {
+    for (uint32_t v = 0; v < kUnpackThreads / 64; ++v)
+      if (v < w) before += cnt[k][v];
+    const uint32_t col = b * kUnpackCols + k * kUnpackThreads + threadIdx.x;
+    if (col < nd) {
+      const uint32_t i = frame_index(d, col, ndev, tile_rays);
+      const uint32_t pos = off + before + (uint32_t)__popcll(bal[k] & below);
+      const bool from_rows = keep[k] && pos < cap;
+#pragma unroll
+      for (uint32_t r = 0; r < 6u; ++r)
+        out_rays[(size_t)r * n + i] = from_rows ? rows[(size_t)r * (cap + 1u) + pos] : prim[(size_t)r * n + i];
+      out_status[i] = byte[k] & 3u;
+      if (out_segments) out_segments[i] = byte[k] >> 2;
+    }
+    for (uint32_t v = w; v < kUnpackThreads / 64; ++v) before += cnt[k][v];
+  }
 }
 
 struct DeviceGuard {
@@ -116,6 +245,18 @@ struct bzr_tiled {
   hipEvent_t done = nullptr;         // device 0: last unpack
   float *host_out = nullptr;         // host-pointer frames: device-0 staging for [6][n] + 2 x [n]
   uint64_t frames = 0;
+  // gather layout (bzr_tiled_set_layout): BZR_PACK_RAYS, or BZR_PACK_COMPACT with `cap` survivors per share
+  int32_t layout = BZR_PACK_RAYS;
+  uint32_t cap = 0, cpad = 0;        // compact: capacity; npad rounded up to a multiple of 4 (byte words)
+  size_t words = 0;                  // floats of one packed share (the allocation: the larger layout)
+  float *prim0 = nullptr;            // device 0: the frame's primary rays [6][n] (bzr_tiled_set_rays)
+  bool prim_valid = false;
+  uint32_t *dshare = nullptr;        // device 0: share sizes [ndev]
+  uint32_t *unpack = nullptr;        // device 0: compact block counts / offsets [2][ndev][nblk], overflow flag
+  uint32_t nblk = 0;                 // compact: 1024-column blocks per share
+  size_t packed_words() const {
+    return layout == BZR_PACK_COMPACT ? (size_t)cpad / 4u + 1u + 6u * ((size_t)cap + 1u) : (size_t)kRows * npad;
+  }
 
   ~bzr_tiled() {
     for (uint32_t d = 0; d < gstream.size(); ++d)
@@ -143,7 +284,12 @@ struct bzr_tiled {
       for (hipEvent_t e : s.packed_ev) if (e) (void)hipEventDestroy(e);
       for (hipEvent_t e : s.sent_ev) if (e) (void)hipEventDestroy(e);
     }
-    if (!dev.empty()) free_on(dev[0], host_out);
+    if (!dev.empty()) {
+      free_on(dev[0], host_out);
+      free_on(dev[0], prim0);
+      free_on(dev[0], dshare);
+      free_on(dev[0], unpack);
+    }
     for (uint32_t d = 0; d < gstream.size(); ++d)
       if (gstream[d]) (void)hipStreamDestroy(gstream[d]);
     if (done) (void)hipEventDestroy(done);
@@ -183,6 +329,9 @@ bzr_status build(bzr_tiled &t, bzr_ctx *const *ctxs, int32_t transport) {
   t.share.assign(ndev, 0);
   for (uint32_t k = 0; k < tiles; ++k) t.share[k % ndev] += std::min(t.tile_rays, t.n - k * t.tile_rays);
   t.npad = ((tiles + ndev - 1) / ndev) * t.tile_rays;
+  t.cpad = (t.npad + 3u) / 4u * 4u;
+  t.words = std::max((size_t)kRows * t.npad, (size_t)t.cpad / 4u + 1u + 6u * ((size_t)t.npad + 1u));
+  t.nblk = (t.npad + kUnpackCols - 1) / kUnpackCols;
 
   t.in.assign(ndev, nullptr);
   for (uint32_t d = 0; d < ndev; ++d)
@@ -199,12 +348,12 @@ bzr_status build(bzr_tiled &t, bzr_ctx *const *ctxs, int32_t transport) {
       if (bzr_status s = alloc_on(t.dev[d], sl.rays[d], (size_t)6 * t.share[d])) return s;
       if (bzr_status s = alloc_on(t.dev[d], sl.status[d], t.share[d])) return s;
       if (bzr_status s = alloc_on(t.dev[d], sl.segments[d], t.share[d])) return s;
-      if (bzr_status s = alloc_on(t.dev[d], sl.packed[d], (size_t)kRows * t.npad)) return s;
+      if (bzr_status s = alloc_on(t.dev[d], sl.packed[d], t.words)) return s;
       DeviceGuard g(t.dev[d]);
       TILED_HIP(hipEventCreateWithFlags(&sl.packed_ev[d], hipEventDisableTiming));
       TILED_HIP(hipEventCreateWithFlags(&sl.sent_ev[d], hipEventDisableTiming));
     }
-    if (bzr_status s = alloc_on(t.dev[0], sl.recv, (size_t)ndev * kRows * t.npad)) return s;
+    if (bzr_status s = alloc_on(t.dev[0], sl.recv, (size_t)ndev * t.words)) return s;
   }
   const uint32_t nstreams = t.transport == BZR_GATHER_RCCL ? ndev : 1u;
   t.gstream.assign(nstreams, nullptr);
@@ -215,6 +364,10 @@ bzr_status build(bzr_tiled &t, bzr_ctx *const *ctxs, int32_t transport) {
   {
     DeviceGuard g(t.dev[0]);
     TILED_HIP(hipEventCreateWithFlags(&t.done, hipEventDisableTiming));
+    if (bzr_status s = alloc_on(t.dev[0], t.dshare, ndev)) return s;
+    if (bzr_status s = alloc_on(t.dev[0], t.unpack, (size_t)2 * ndev * t.nblk + 1)) return s;
+    TILED_HIP(hipMemcpy(t.dshare, t.share.data(), ndev * sizeof(uint32_t), hipMemcpyHostToDevice));
+    TILED_HIP(hipMemset(t.unpack + (size_t)2 * ndev * t.nblk, 0, sizeof(uint32_t)));
   }
   if (t.transport == BZR_GATHER_RCCL) {
     t.comm.assign(ndev, nullptr);
@@ -275,6 +428,7 @@ extern "C" bzr_status bzr_tiled_share_rays(bzr_tiled *t, uint32_t d, float **ray
   if (!t || !rays_soa) return fail(BZR_ERR_INVALID_ARGUMENT, "bzr_tiled_share_rays: null argument");
   if (d >= t->ndev) return fail(BZR_ERR_INVALID_ARGUMENT, "bzr_tiled_share_rays: device index out of range");
   *rays_soa = t->in[d];
+  t->prim_valid = false;  // the caller writes the shares: device 0's copy of the frame is no longer known good
   return BZR_OK;
 }
 
@@ -298,6 +452,25 @@ extern "C" bzr_status bzr_tiled_set_rays(bzr_tiled *t, const float *rays, uint32
     }
     src0 = stage0;
   }
+  // device 0 keeps the whole frame: the compact layout returns a ray that never refracted from it
+  if (!t->prim0)
+    if (bzr_status s = alloc_on(t->dev[0], t->prim0, (size_t)6 * t->n)) {
+      if (stage0) {
+        DeviceGuard g(t->dev[0]);
+        (void)hipFree(stage0);
+      }
+      return s;
+    }
+  {
+    DeviceGuard g(t->dev[0]);
+    hipError_t e = hipMemcpyAsync(t->prim0, src0, bytes, hipMemcpyDeviceToDevice, c0->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c0->stream);
+    if (e != hipSuccess) {
+      if (stage0) (void)hipFree(stage0);
+      return fail(BZR_ERR_HIP, std::string("bzr_tiled_set_rays: ") + hipGetErrorString(e));
+    }
+  }
+  t->prim_valid = true;
   bzr_status result = BZR_OK;
   for (uint32_t d = 0; d < t->ndev && result == BZR_OK; ++d) {
     if (t->share[d] == 0) continue;
@@ -336,7 +509,7 @@ namespace {
 
 bzr_status gather_and_unpack(bzr_tiled &t, bzr_tiled::Slot &sl, float *out_rays, uint32_t *out_status,
                              uint32_t *out_segments) {
-  const size_t count = (size_t)kRows * t.npad;
+  const size_t count = t.packed_words(), stride = t.words;
   if (t.transport == BZR_GATHER_RCCL) {
     for (uint32_t d = 0; d < t.ndev; ++d) {
       DeviceGuard g(t.dev[d]);
@@ -345,7 +518,7 @@ bzr_status gather_and_unpack(bzr_tiled &t, bzr_tiled::Slot &sl, float *out_rays,
     TILED_NCCL(ncclGroupStart());
     for (uint32_t d = 0; d < t.ndev; ++d) {
       ncclResult_t r = ncclSend(sl.packed[d], count, ncclFloat32, 0, t.comm[d], t.gstream[d]);
-      if (r == ncclSuccess) r = ncclRecv(sl.recv + (size_t)d * count, count, ncclFloat32, static_cast<int>(d), t.comm[0],
+      if (r == ncclSuccess) r = ncclRecv(sl.recv + (size_t)d * stride, count, ncclFloat32, static_cast<int>(d), t.comm[0],
                                          t.gstream[0]);
       if (r != ncclSuccess) {
         (void)ncclGroupEnd();
@@ -361,14 +534,24 @@ bzr_status gather_and_unpack(bzr_tiled &t, bzr_tiled::Slot &sl, float *out_rays,
     DeviceGuard g(t.dev[0]);
     for (uint32_t d = 0; d < t.ndev; ++d) {
       TILED_HIP(hipStreamWaitEvent(t.gstream[0], sl.packed_ev[d], 0));
-      TILED_HIP(hipMemcpyPeerAsync(sl.recv + (size_t)d * count, t.dev[0], sl.packed[d], t.dev[d], count * sizeof(float),
+      TILED_HIP(hipMemcpyPeerAsync(sl.recv + (size_t)d * stride, t.dev[0], sl.packed[d], t.dev[d], count * sizeof(float),
                                    t.gstream[0]));
     }
     for (uint32_t d = 0; d < t.ndev; ++d) TILED_HIP(hipEventRecord(sl.sent_ev[d], t.gstream[0]));
   }
   DeviceGuard g(t.dev[0]);
-  hipLaunchKernelGGL(k_tiled_unpack, dim3((t.n + kThreads - 1) / kThreads), dim3(kThreads), 0, t.gstream[0], sl.recv,
-                     t.ndev, t.npad, t.tile_rays, t.n, out_rays, out_status, out_segments);
+  if (t.layout == BZR_PACK_COMPACT) {
+    uint32_t *bc = t.unpack, *bo = t.unpack + (size_t)t.ndev * t.nblk, *flag = t.unpack + (size_t)2 * t.ndev * t.nblk;
+    const dim3 grid(t.ndev * t.nblk);
+    hipLaunchKernelGGL(k_unpack_count, grid, dim3(kUnpackThreads), 0, t.gstream[0], sl.recv, stride, t.dshare, t.nblk, bc);
+    hipLaunchKernelGGL(k_unpack_scan, dim3(t.ndev), dim3(kUnpackScan), 0, t.gstream[0], sl.recv, stride, t.cpad, t.cap,
+                       t.dshare, t.nblk, bc, bo, flag);
+    hipLaunchKernelGGL(k_unpack_compact, grid, dim3(kUnpackThreads), 0, t.gstream[0], sl.recv, stride, t.cpad, t.cap,
+                       t.dshare, t.nblk, bo, t.prim0, t.ndev, t.tile_rays, t.n, out_rays, out_status, out_segments);
+  } else {
+    hipLaunchKernelGGL(k_tiled_unpack, dim3((t.n + kThreads - 1) / kThreads), dim3(kThreads), 0, t.gstream[0], sl.recv,
+                       stride, t.ndev, t.npad, t.tile_rays, t.n, out_rays, out_status, out_segments);
+  }
   TILED_HIP(hipGetLastError());
   TILED_HIP(hipEventRecord(t.done, t.gstream[0]));
   return BZR_OK;
@@ -382,6 +565,9 @@ extern "C" bzr_status bzr_tiled_trace(bzr_tiled *t, const bzr_mesh *const *lense
   if (!lenses || !ri || nlens == 0) return fail(BZR_ERR_INVALID_ARGUMENT, "bzr_tiled_trace: null lens list");
   if (!out_rays || !out_status) return fail(BZR_ERR_INVALID_ARGUMENT, "bzr_tiled_trace: null output");
   const bool host = !(flags & BZR_DEVICE_PTRS);
+  if (t->layout == BZR_PACK_COMPACT && !t->prim_valid)
+    return fail(BZR_ERR_INVALID_ARGUMENT, "bzr_tiled_trace: the compact layout needs the frame's rays through "
+                                          "bzr_tiled_set_rays (device 0 returns the rays that never refracted)");
   const uint32_t s = static_cast<uint32_t>(t->frames % t->nslot);
   bzr_tiled::Slot &sl = t->slot[s];
   for (uint32_t d = 0; d < t->ndev; ++d) {
@@ -394,8 +580,9 @@ extern "C" bzr_status bzr_tiled_trace(bzr_tiled *t, const bzr_mesh *const *lense
     DeviceGuard g(t->dev[d]);
     if (sl.used) TILED_HIP(hipStreamWaitEvent(c->stream, sl.sent_ev[d], 0));  // the previous gather left the buffer
     if (t->share[d]) {
-      bzr_status st = bzr_pack_frame(c, BZR_PACK_RAYS, sl.rays[d], sl.status[d], sl.segments[d], t->share[d], t->npad, 0,
-                                     sl.packed[d]);
+      const bool compact = t->layout == BZR_PACK_COMPACT;
+      bzr_status st = bzr_pack_frame(c, t->layout, sl.rays[d], sl.status[d], sl.segments[d], t->share[d],
+                                     compact ? t->cpad : t->npad, compact ? t->cap : 0u, sl.packed[d]);
       if (st != BZR_OK) return fail(st, "bzr_tiled_trace: pack, device " + std::to_string(d) + ": " + bzr_last_error());
     }
     TILED_HIP(hipEventRecord(sl.packed_ev[d], c->stream));
@@ -437,7 +624,70 @@ extern "C" bzr_status bzr_tiled_sync(bzr_tiled *t) {
   }
   for (bzr_ctx *c : t->ctxs)
     if (bzr_status s = bzr_sync(c)) return s;
+  if (t->unpack) {  // a compact frame whose survivors exceeded the capacity since the last sync
+    DeviceGuard g(t->dev[0]);
+    uint32_t *flag = t->unpack + (size_t)2 * t->ndev * t->nblk, h = 0;
+    TILED_HIP(hipMemcpy(&h, flag, sizeof(h), hipMemcpyDeviceToHost));
+    if (h) {
+      TILED_HIP(hipMemset(flag, 0, sizeof(h)));
+      return fail(BZR_ERR_CAPACITY, "bzr_tiled_sync: a frame had more survivors than the compact capacity " +
+                                        std::to_string(t->cap) + ": its outputs are incomplete (bzr_tiled_calibrate or a "
+                                        "larger cap)");
+    }
+  }
   return BZR_OK;
+}
+
+extern "C" bzr_status bzr_tiled_set_layout(bzr_tiled *t, int32_t layout, uint32_t cap) {
+  if (!t) return fail(BZR_ERR_INVALID_ARGUMENT, "bzr_tiled_set_layout: null plan");
+  if (layout != BZR_PACK_RAYS && layout != BZR_PACK_COMPACT)
+    return fail(BZR_ERR_INVALID_ARGUMENT, "bzr_tiled_set_layout: BZR_PACK_RAYS or BZR_PACK_COMPACT");
+  if (layout == BZR_PACK_COMPACT && (cap == 0 || cap > t->npad))
+    return fail(BZR_ERR_INVALID_ARGUMENT, "bzr_tiled_set_layout: compact needs 0 < cap <= npad (" + std::to_string(t->npad) + ")");
+  if (bzr_status s = bzr_tiled_sync(t)) return s;  // frames in flight finish under the old layout
+  t->layout = layout;
+  t->cap = layout == BZR_PACK_COMPACT ? cap : 0u;
+  return BZR_OK;
+}
+
+extern "C" bzr_status bzr_tiled_calibrate(bzr_tiled *t, const bzr_mesh *const *lenses, const float *ri, uint32_t nlens,
+                                          uint32_t flags, uint32_t *cap_out) {
+  if (!t) return fail(BZR_ERR_INVALID_ARGUMENT, "bzr_tiled_calibrate: null plan");
+  if (!t->prim_valid)
+    return fail(BZR_ERR_INVALID_ARGUMENT, "bzr_tiled_calibrate: set the frame's rays first (bzr_tiled_set_rays)");
+  if (bzr_status s = bzr_tiled_set_layout(t, BZR_PACK_RAYS, 0)) return s;
+  float *o = nullptr;
+  uint32_t *cnt = nullptr;
+  if (bzr_status s = alloc_on(t->dev[0], o, (size_t)8 * t->n)) return s;
+  bzr_status s = alloc_on(t->dev[0], cnt, t->ndev);
+  uint32_t *st = reinterpret_cast<uint32_t *>(o + (size_t)6 * t->n), *sg = st + t->n;
+  if (s == BZR_OK) s = bzr_tiled_trace(t, lenses, ri, nlens, o, st, sg, flags | BZR_DEVICE_PTRS);
+  std::vector<uint32_t> h(t->ndev, 0u);
+  if (s == BZR_OK) {
+    DeviceGuard g(t->dev[0]);
+    hipStream_t gs = t->gstream[0];
+    hipError_t e = hipMemsetAsync(cnt, 0, t->ndev * sizeof(uint32_t), gs);
+    if (e == hipSuccess) {
+      hipLaunchKernelGGL(k_count_survivors, dim3((t->n + kThreads - 1) / kThreads), dim3(kThreads), 0, gs, st, sg, t->n,
+                         t->ndev, t->tile_rays, cnt);
+      e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(h.data(), cnt, t->ndev * sizeof(uint32_t), hipMemcpyDeviceToHost, gs);
+    if (e == hipSuccess) e = hipStreamSynchronize(gs);
+    if (e != hipSuccess) s = fail(BZR_ERR_HIP, std::string("bzr_tiled_calibrate: ") + hipGetErrorString(e));
+  }
+  if (s == BZR_OK) s = bzr_tiled_sync(t);
+  {
+    DeviceGuard g(t->dev[0]);
+    (void)hipFree(o);
+    if (cnt) (void)hipFree(cnt);
+  }
+  if (s != BZR_OK) return s;
+  // the largest share's survivors + 1/64 + 64 rays of headroom (bench.py's rule, frame.compact_capacity)
+  const uint32_t most = *std::max_element(h.begin(), h.end());
+  const uint32_t cap = static_cast<uint32_t>(std::min<uint64_t>(t->npad, (uint64_t)most + most / 64u + 64u));
+  if (cap_out) *cap_out = cap;
+  return bzr_tiled_set_layout(t, BZR_PACK_COMPACT, cap);
 }
 
 // The one-call form (include/bzr.h): a one-slot plan over ctxs for this frame only.  Host pointers: results

@@ -179,6 +179,12 @@ void TiledChain::trace(Ray *outRays, RefractionResult *outStatus, uint32_t *outS
   }
 }
 
+uint32_t TiledChain::calibrate(uint32_t flags) {
+  uint32_t cap = 0;
+  check(bzr_tiled_calibrate(mPlan, mMeshes.data(), mRi.data(), static_cast<uint32_t>(mRi.size()), flags, &cap));
+  return cap;
+}
+
 void TiledChain::sync() { check(bzr_tiled_sync(mPlan)); }
 
 }  // namespace bzr

@@ -66,7 +66,8 @@ enum {
   BZR_ERR_HIP = 2,
   BZR_ERR_OUT_OF_MEMORY = 3,
   BZR_ERR_PREPROCESS = 4,   /* a reference preprocessing "throw" (e.g. "Vertex on edge detected.") */
-  BZR_ERR_NO_DEVICE = 5
+  BZR_ERR_NO_DEVICE = 5,
+  BZR_ERR_CAPACITY = 6      /* a compact multi-GPU gather had more survivors than its capacity (bzr_tiled_sync) */
 };
 
 enum {
@@ -245,7 +246,19 @@ bzr_status bzr_tiled_trace(bzr_tiled *plan, const bzr_mesh *const *lenses, const
                            uint32_t flags);
 /* Device 0's gather stream: the outputs of the last bzr_tiled_trace are complete in its order. */
 bzr_status bzr_tiled_stream(bzr_tiled *plan, void **hip_stream);
+/* Waits for every frame queued; returns BZR_ERR_CAPACITY if a compact frame since the last sync had more
+ * survivors than the capacity (that frame's outputs are incomplete). */
 bzr_status bzr_tiled_sync(bzr_tiled *plan);
+/* What each device sends per frame (bzr_pack_frame's layouts): BZR_PACK_RAYS (default; 28 B per ray of the
+ * share, npad columns) or BZR_PACK_COMPACT: one status/segment byte per ray, the survivor count and the
+ * final rays of at most `cap` survivors (the rays that refracted at least once; 0 < cap <= npad) -- device
+ * 0 returns the others' primary rays from its copy of the frame, so the compact layout needs
+ * bzr_tiled_set_rays.  Synchronises first. */
+bzr_status bzr_tiled_set_layout(bzr_tiled *plan, int32_t layout, uint32_t cap);
+/* Traces one frame (rays layout, synchronous), counts each device's survivors and switches to the compact
+ * layout with cap = the largest count + 1/64 + 64 (at most npad); cap_out (may be NULL) gets it. */
+bzr_status bzr_tiled_calibrate(bzr_tiled *plan, const bzr_mesh *const *lenses, const float *refractive_index,
+                               uint32_t nlens, uint32_t flags, uint32_t *cap_out);
 /* BezierMesh::interpolate(divisor) on the device (reference/bezierMesh.cpp:55-66): the tessellated
  * surface, divisor^2 sub-triangles of every patch, in the reference's order (sub-triangle outer,
  * patch inner).  out_xyz: divisor^2 * n_patches triangles x 3 vertices x 3 floats.  divisor >= 1.

@@ -465,6 +465,9 @@ class TiledChain {
   void setRaysDevice(float const *raysSoaOnDevice0);      // [6][n] SoA on slot 0 device 0
   void trace(float *outRaysSoa, uint32_t *outStatus, uint32_t *outSegments = nullptr, uint32_t flags = 0);  // device 0
   void trace(Ray *outRays, RefractionResult *outStatus, uint32_t *outSegments = nullptr, uint32_t flags = 0);  // host
+  // Compact gather (bzr_tiled_calibrate): one counted frame, then only the refracted rays cross to device 0
+  // (needs setRays); returns the capacity.  sync() throws if a later frame exceeds it.
+  uint32_t calibrate(uint32_t flags = 0);
   void sync();
 
  private:

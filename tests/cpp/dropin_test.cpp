@@ -297,7 +297,8 @@ static void hot_path(Mesh const &lensMesh) {
     bzr::TiledChain frames({{&s00, &s01}, {&s10, &s11}}, {&lens}, n, 512);
     CHECK(frames.transport() == BZR_GATHER_PEER);
     frames.setRays(rays.data());
-    for (int k = 0; k < 3; ++k) {
+    for (int k = 0; k < 4; ++k) {
+      if (k == 2) CHECK(frames.calibrate() > 0u);  // the last two frames gather only the refracted rays
       std::vector<Ray> o(n);
       std::vector<RefractionResult> so(n);
       std::vector<uint32_t> sg(n);

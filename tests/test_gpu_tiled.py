@@ -131,3 +131,59 @@ def test_tiled_plan_share_rays_and_host_outputs(bzr, ctx):
     lenses = [[bzr.DeviceMesh(c, p) for p in patches] for c in slots[0]]
     plan.trace(lenses, ri, *out)
     _same(out, bzr.trace_chain(ctx, [bzr.DeviceMesh(ctx, p) for p in patches], ri, rays))
+
+
+@pytest.mark.parametrize("transport,ndev", [("peer", 3), ("rccl", 1)])
+def test_tiled_plan_compact_gather(bzr, ctx, transport, ndev):
+    """The compact layout (bzr_tiled_calibrate: one counted frame, then survivors only up to a capacity):
+    frames bit-identical to one bzr_trace_chain, the rays that never refracted returned from device 0's copy
+    of the frame; a capacity below the survivors is reported by bzr_tiled_sync (BZR_ERR_CAPACITY)."""
+    import torch
+
+    cfg, patches, ri = _cfg4(bzr)
+    rays = grid_rays(cfg, side=256)
+    n = rays.shape[1]
+    tp = {"peer": bzr.GATHER_PEER, "rccl": bzr.GATHER_RCCL}[transport]
+    slots = [[bzr.Context(0) for _ in range(ndev)] for _ in range(2)]
+    lenses = [[bzr.DeviceMesh(c, p) for p in patches] for c in slots[0]]
+    plan = bzr.TiledPlan(slots, n, tile_rays=4096, transport=tp)
+    plan.set_rays(torch.from_numpy(rays).cuda())
+    want = bzr.trace_chain(ctx, [bzr.DeviceMesh(ctx, p) for p in patches], ri, rays)
+    survivors = int(((want[2] >= 2) | (want[1] != 0)).sum())
+    cap = plan.calibrate(lenses, ri)
+    _, share, npad = plan.info()
+    assert 0 < cap <= npad and cap * ndev >= survivors
+    outs = [(torch.empty((6, n), device="cuda"), torch.empty(n, dtype=torch.int32, device="cuda"),
+             torch.empty(n, dtype=torch.int32, device="cuda")) for _ in range(4)]
+    for o in outs:
+        plan.trace(lenses, ri, *o)
+    plan.sync()
+    for o in outs:
+        _same(o, want)
+    # host outputs through the same layout
+    ho = (np.empty((6, n), np.float32), np.empty(n, np.uint32), np.empty(n, np.uint32))
+    plan.trace(lenses, ri, *ho)
+    _same(ho, want)
+    # too small a capacity: the frame is incomplete and sync says so
+    plan.set_layout("compact", cap=64)
+    plan.trace(lenses, ri, *outs[0])
+    with pytest.raises(bzr.BzrError, match="capacity"):
+        plan.sync()
+    plan.sync()  # the flag was reported once
+    plan.close()
+
+
+def test_tiled_plan_compact_needs_the_frame_rays(bzr, ctx):
+    """Rays written into the shares directly leave device 0 without the frame: compact frames are refused."""
+    import ctypes
+
+    cfg, patches, ri = _cfg4(bzr)
+    slots = [[bzr.Context(0) for _ in range(2)]]
+    plan = bzr.TiledPlan(slots, 8192, tile_rays=4096, transport=bzr.GATHER_PEER)
+    p = ctypes.c_void_p()
+    bzr._check(bzr.lib().bzr_tiled_share_rays(plan.handle, 0, ctypes.byref(p)))
+    plan.set_layout("compact", cap=4096)
+    lenses = [[bzr.DeviceMesh(c, q) for q in patches] for c in slots[0]]
+    out = (np.empty((6, 8192), np.float32), np.empty(8192, np.uint32), np.empty(8192, np.uint32))
+    with pytest.raises(bzr.BzrError, match="set_rays"):
+        plan.trace(lenses, ri, *out)
