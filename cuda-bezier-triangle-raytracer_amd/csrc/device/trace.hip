@@ -1156,7 +1156,20 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
 #ifndef BZR_TRAV_XCD
 #define BZR_TRAV_XCD 1
 #endif
-__global__ __launch_bounds__(kTravBlock) void k_traverse(MeshView m, const float *__restrict__ rays, uint32_t ld,
+// BZR_TRAV_WPE (default 8; 0 = the compiler's choice, 7 waves): amdgpu_waves_per_eu lower bound for k_traverse.
+// At 8 waves per SIMD it keeps 64 VGPRs (35 SGPRs spill into VGPR lanes, no scratch): its walk waits on memory
+// 45 % of its cycles, and the eighth wave hides more of it -- k_traverse -8 % on cfg5 (4.91 -> 4.52 ms per
+// frame) and -10 % on cfg3 (0.221 -> 0.200 ms), frames -4.2 / -4.8 %, same bits (two box runs agree;
+// profiles/r04_ab_traverse_wpe8.jsonl).
+#ifndef BZR_TRAV_WPE
+#define BZR_TRAV_WPE 8
+#endif
+#if BZR_TRAV_WPE
+#define BZR_TRAV_ATTR __attribute__((amdgpu_waves_per_eu(BZR_TRAV_WPE)))
+#else
+#define BZR_TRAV_ATTR
+#endif
+__global__ __launch_bounds__(kTravBlock) BZR_TRAV_ATTR void k_traverse(MeshView m, const float *__restrict__ rays, uint32_t ld,
                                                          uint32_t off, const uint32_t *__restrict__ alive, uint32_t n,
                                                          Work w, unsigned long long *counters) {
   __shared__ uint32_t stack[kTravBlock / 64][kStack];
@@ -1331,6 +1344,9 @@ __global__ __launch_bounds__(kBlock) void k_finish(MeshView m, const float *rays
   if (i >= n) return;
   const uint32_t gi = off + i;
   if (kMode == kModeStage && !o.first && o.status[gi] == BZR_RR_NONE) return;
+  // the ray is loaded unconditionally: making the load depend on w.count (an intersect chunk's hits need it
+  // only for an overflow ray) serialises the two reads and measured slower (cfg3 k_finish 0.059 -> 0.069 ms,
+  // profiles/r04_ab_traverse_wpe8.jsonl, variant "finish")
   f3 s, d;
   load_ray(rays, ld, gi, s, d);
   Hit h = no_hit();
