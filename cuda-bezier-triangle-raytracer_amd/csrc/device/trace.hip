@@ -181,17 +181,28 @@ constexpr int kTravBlock = BZR_TRAV_BLOCK;
 #ifndef BZR_NEWTON_GATED
 #define BZR_NEWTON_GATED 1
 #endif
-// A 64-pair chunk with more distinct patches than this goes to k_newton_lane (one record per lane).
 // BZR_STAGED_AOS (default 0): k_traverse also writes each ray of the chunk as a 32-byte AoS record (ox oy oz dx
 // | dy dz), and the Newton / resolve kernels read a pair's ray from it -- one 32-byte sector instead of six
 // SoA rows whose 128-byte lines serve few of a bucket's rays.
 #ifndef BZR_STAGED_AOS
 #define BZR_STAGED_AOS 0
 #endif
-#ifndef BZR_LANE_THRESHOLD
-#define BZR_LANE_THRESHOLD 3
+// BZR_DENSE_MIN (default 16): the staged pair layout.  A patch bucket's pairs fill whole 64-pair chunks of
+// that one patch (dense chunks: patch-uniform Newton passes, every lane busy); its last, partial chunk is
+// padded to a whole chunk when it holds at least this many pairs, else its pairs go to the sparse region
+// behind the dense chunks, where k_newton_lane runs one pair per lane with the lane's own patch record.
+// 64 = no padding.  (A sparse chunk costs ~4 dense ones -- 4 waves per SIMD, per-lane record loads -- so a
+// remainder of r pairs is cheaper padded from r ~ 16 on; cfg5: DESIGN.md.)  Padding is below 64 slots per
+// patch, which sizes the pair array at cap + 64 (nb + 1).
+#ifndef BZR_DENSE_MIN
+#define BZR_DENSE_MIN 16
 #endif
-constexpr uint32_t kLaneThreshold = BZR_LANE_THRESHOLD;
+constexpr uint32_t kDenseMin = BZR_DENSE_MIN;
+static_assert(kDenseMin >= 1 && kDenseMin <= 64, "BZR_DENSE_MIN: 1..64");
+// Staged winner keys (t order << 32 | patch << 6 | list slot j) and pair records (ray | j << 26,
+// patch | follow side << 30): chunk rays below 2^26, list slots below 64, patch indices below 2^25 (keys
+// take 26 bits; the pair array's 32-bit indices, 64 padding slots per patch).
+constexpr uint32_t kStagedPatchLimit = 1u << 25, kRayMask = (1u << 26) - 1u, kNoPair = 0xFFFFFFFFu;
 struct MeshView {
   const float4 *__restrict__ planar;
   const float *__restrict__ full;
@@ -467,31 +478,34 @@ __device__ __forceinline__ void node_children(const bzr_host::Bvh4Node *nodes, c
 //   k_traverse  BVH walk, exact planar gate -> up to kMaxCand candidates per ray, a per-patch
 //               histogram (rank of each (ray, patch) pair within its patch bucket) and the list
 //               of rays that need the full scan (list/stack overflow, origin beyond s_max)
-//   scan        exclusive sum of the histogram (hipCUB) -> bucket offsets, total pair count
-//   k_scatter   (ray, patch) pairs into patch-major order (8-byte records: the Newton stage reads the
-//               ray itself from the ray array -- neighbouring rays, mostly cached -- instead of a 32-byte
-//               copy travelling with the pair)
-//   k_newton    the Newton stage per pair; a wave holds <= a few distinct patches, processed one at a
-//               time with the patch record in scalar registers (uniform loads); hits go to a per-pair
-//               slot and a per-ray 64-bit atomicMin on (t order key, pair index)
+//   scan        exclusive sum over the buckets of (dense chunks << 32 | sparse pairs) (bucket_split;
+//               hipCUB or k_scan_small) -> each bucket's dense chunk and sparse offsets, the totals
+//   k_place     (ray, patch) pair records into their bucket's dense chunks or the sparse region (8-byte
+//               records: the Newton stage reads the ray itself from the ray array -- neighbouring rays,
+//               mostly cached -- instead of a 32-byte copy travelling with the pair); marks the padded
+//               lanes of each bucket's last dense chunk; clears the histogram for the next segment
+//   k_newton    the Newton stage over the dense chunks: one patch per chunk, its record in scalar
+//               registers (uniform loads); hits go to the ray's list slot and a per-ray 64-bit atomicMin
+//               on (t order, patch, slot)
+//   k_newton_lane  the sparse region: one pair per lane, the lane's own patch record
 //   k_resolve   follow-side results: the named neighbour with cNone, per lane; then the reference's
 //               in-order scan for the overflow list, sliced over patches -> key
 //   k_finish    winner -> BezierIntersection / refraction (overflow rays: their winner re-evaluated)
-// Pair indices are patch-major, so for one ray (t, pair index) orders like (t, scanned patch
-// index): the atomicMin winner is the reference's strict-< in-order winner.
+// For one ray (t order, patch, slot) orders like (t, scanned patch index): the atomicMin winner is the
+// reference's strict-< in-order winner (record()).
 struct Work {
-  uint32_t *ctr;     // [0] follow count, [1] overflow count, [2] rays traced, [3] k_newton_lane chunks
+  uint32_t *ctr;     // [0] follow count, [1] overflow count, [2] rays traced, [3] pairs listed
   uint32_t *hist;    // [nb + 1] pair counts per patch (hist[nb] = 0); 256 bytes after ctr
-  uint32_t *offs;    // [nb + 1] exclusive prefix of hist; offs[nb] = pair count
+  unsigned long long *offs;  // [nb + 1] exclusive prefix of bucket_split(hist); offs[nb] = the totals
   uint32_t *cand;    // [kMaxCand][n]
   uint32_t *rank;    // [kMaxCand][n]
   uint32_t *count;   // [n]
   unsigned long long *key;  // [n]
-  float *slot;       // [cap][kSlotWords] per-pair hit (AoS, 48 bytes)
-  uint2 *pairs;      // [cap] pair records (ray, patch); the Newton stage reads the ray from the ray array
-  uint32_t *fol;     // [cap] pair | what << 30
+  float *slot;       // [kMaxCand][n] x kSlotWords: the hit of ray i's list slot j at j * n + i (AoS, 48 bytes)
+  uint2 *pairs;      // [cap + 64 (nb + 1)] pair records (ray | j << 26, patch): dense chunks, then the sparse
+                     // region; a follow request adds its side << 30 to the patch word
+  uint32_t *fol;     // [cap] follow requests: pair indices
   uint32_t *ovf;     // [n]
-  uint32_t *lanes;   // [cap / 64 + 1] chunks for k_newton_lane (count in ctr[3])
   float4 *aos;       // [2 * chunk] the chunk's rays as 32-byte records (BZR_STAGED_AOS)
   void *cub;
   size_t cub_bytes;
@@ -546,15 +560,19 @@ __device__ __forceinline__ uint32_t lanes_below(unsigned long long mask) {
 
 // One intersecting pair result: its slot, then the ray's running (t, pair) minimum.  t that cannot
 // beat the reference's initial FLT_MAX (NaN, FLT_MAX, +inf) is dropped; -0 ties with +0.
-__device__ __forceinline__ void record(float *__restrict__ slot, uint32_t cap, uint32_t p, const Hit &h, uint32_t src,
-                                       unsigned long long *key) {
-  (void)cap;
+// A staged hit of ray `ray`'s list slot j (candidate patch b; the hit itself may be b's neighbour src after a
+// follow): its 48-byte record goes to slot j * n + ray, and the ray's key takes the lexicographic minimum of
+// (t order, b, j).  A ray's candidates are distinct patches, so for one ray that orders like the reference's
+// (t, scanned patch index) with strict < -- the follow side's hit ranks at its candidate's position, as in
+// reference/bezierMesh.cpp:206-227 (oracle orc_mesh_intersect).
+__device__ __forceinline__ void record(float *__restrict__ slot, uint32_t n, uint32_t ray, uint32_t j, uint32_t b,
+                                       const Hit &h, uint32_t src, unsigned long long *key) {
   if (!(h.t < FLT_MAX)) return;
-  float4 *r = reinterpret_cast<float4 *>(slot) + (size_t)3 * p;  // AoS: 48 bytes per pair
+  float4 *r = reinterpret_cast<float4 *>(slot) + (size_t)3 * ((size_t)j * n + ray);  // AoS: 48 bytes per slot
   r[0] = make_float4(h.t, h.point.x, h.point.y, h.point.z);
   r[1] = make_float4(h.cs, h.bary.x, h.bary.y, h.bary.z);
   r[2] = make_float4(h.normal.x, h.normal.y, h.normal.z, __uint_as_float(src));
-  atomicMin(key, ((unsigned long long)t_order(h.t) << 32) | p);
+  atomicMin(key, ((unsigned long long)t_order(h.t) << 32) | (b << 6) | j);
 }
 
 // Word group g of a 64-byte leaf record (planar record, patch index in the last word): q0..q3 of the gate.
@@ -1192,19 +1210,49 @@ __global__ __launch_bounds__(kTravBlock) BZR_TRAV_ATTR void k_traverse(MeshView 
 }
 
 
-__global__ __launch_bounds__(kBlock) void k_scatter(const float *__restrict__ rays, uint32_t ld, uint32_t off,
-                                                    uint32_t n, Work w) {
-  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  if (i >= n) return;
-  (void)rays;
-  (void)ld;
-  (void)off;
-  uint32_t c = w.count[i];
-  if (c > kMaxCand || c == 0) return;
-  for (uint32_t j = 0; j < c; ++j) {
-    const uint32_t b = w.cand[(size_t)j * n + i];
-    const uint32_t p = w.offs[b] + w.rank[(size_t)j * n + i];
-    w.pairs[p] = make_uint2(i, b);
+// A bucket of c pairs in the staged layout (BZR_DENSE_MIN): (dense chunks << 32) | pairs in the sparse region.
+struct BucketSplit {
+  __host__ __device__ __forceinline__ unsigned long long operator()(uint32_t c) const {
+    const uint32_t rem = c & 63u;
+    const bool pad = rem >= kDenseMin;
+    return ((unsigned long long)((c >> 6) + (pad ? 1u : 0u)) << 32) | (pad ? 0u : rem);
+  }
+};
+
+// Threads t < nb: bucket t's padded lanes (the last dense chunk's lanes past its pairs) get the kNoPair
+// record, its histogram word is cleared for the next segment, and (pair_count: with device counters on) the
+// wave adds its buckets' pair counts to ctr[3].  Threads t < n: ray t's listed pairs go to their places -- rank r of bucket b is dense pair
+// 64 dense_base(b) + r while r < 64 dense_chunks(b), else sparse pair r - 64 dense_chunks(b) of the bucket.
+__global__ __launch_bounds__(kBlock) void k_place(uint32_t n, uint32_t nb, Work w, uint32_t *__restrict__ pair_count) {
+  const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+  uint32_t c = 0;
+  if (t < nb) {
+    c = w.hist[t];
+    if (c) {
+      w.hist[t] = 0u;
+      if ((c & 63u) >= kDenseMin) {
+        const uint32_t p0 = static_cast<uint32_t>(w.offs[t] >> 32) * 64u + c, p1 = (p0 + 63u) & ~63u;
+        for (uint32_t p = p0; p < p1; ++p) w.pairs[p] = make_uint2(kNoPair, t);
+      }
+    }
+  }
+  if (pair_count) {  // the wave's listed pairs (bzr_ctx_counters "pairs")
+    uint32_t sum = c;
+#pragma unroll
+    for (int k = 32; k >= 1; k >>= 1) sum += __shfl_xor(sum, k, 64);
+    if ((threadIdx.x & 63u) == 0u && sum) atomicAdd(pair_count, sum);
+  }
+  if (t >= n) return;
+  const uint32_t cnt = w.count[t];
+  if (cnt > kMaxCand || cnt == 0) return;
+  const unsigned long long tot = w.offs[nb];
+  const uint32_t sparse0 = static_cast<uint32_t>(tot >> 32) * 64u;  // the sparse region's first pair
+  for (uint32_t j = 0; j < cnt; ++j) {
+    const uint32_t b = w.cand[(size_t)j * n + t], r = w.rank[(size_t)j * n + t];
+    const unsigned long long o0 = w.offs[b], o1 = w.offs[b + 1];
+    const uint32_t dbase = static_cast<uint32_t>(o0 >> 32), dlen = 64u * (static_cast<uint32_t>(o1 >> 32) - dbase);
+    const uint32_t p = r < dlen ? dbase * 64u + r : sparse0 + static_cast<uint32_t>(o0) + (r - dlen);
+    w.pairs[p] = make_uint2(t | (j << 26), b);
   }
 }
 
@@ -1220,10 +1268,10 @@ __device__ __forceinline__ void flush_follow(uint32_t *buf, uint32_t &nf, uint32
   nf = 0;
 }
 
-// Persistent waves: wave g takes 64-pair chunks g, g + W, ... and fetches the next chunk's pair
-// records while it computes the current one.  A chunk holds few distinct patches (buckets are
-// contiguous); each is processed with its record in scalar registers, `full` being a __restrict__
-// constant-address-space read.
+// Persistent waves over the dense chunks: wave g takes chunks g, g + W, ... and fetches the next chunk's
+// pair records while it computes the current one.  A dense chunk holds one patch (its lane 0 always a real
+// pair), processed with the record in scalar registers, `full` being a __restrict__ constant-address-space
+// read; the padded lanes of a bucket's last chunk (kNoPair) idle.
 // BZR_NEWTON_WPE (default 8): amdgpu_waves_per_eu lower bound for k_newton.  At 8 waves per SIMD the
 // compiler spills ~33 SGPRs to VGPR lanes and keeps 64 VGPRs; measured 2.4 % faster per frame than
 // the unconstrained 7 waves (66 VGPRs, 106 SGPRs), same output bits.
@@ -1232,64 +1280,49 @@ __device__ __forceinline__ void flush_follow(uint32_t *buf, uint32_t &nf, uint32
 #endif
 #define BZR_NEWTON_ATTR __attribute__((amdgpu_waves_per_eu(BZR_NEWTON_WPE)))
 template <bool kFast>
-__global__ __launch_bounds__(kBlock) BZR_NEWTON_ATTR void k_newton(const float *__restrict__ full, const uint32_t *__restrict__ total,
-                                                   const uint2 *__restrict__ pairs, const float *__restrict__ rays,
-                                                   uint32_t ld, uint32_t off, float *__restrict__ slot,
-                                                   uint32_t cap, unsigned long long *__restrict__ key,
+__global__ __launch_bounds__(kBlock) BZR_NEWTON_ATTR void k_newton(const float *__restrict__ full,
+                                                   const unsigned long long *__restrict__ total,
+                                                   uint2 *__restrict__ pairs, const float *__restrict__ rays,
+                                                   uint32_t ld, uint32_t off, uint32_t n, float *__restrict__ slot,
+                                                   unsigned long long *__restrict__ key,
                                                    uint32_t *__restrict__ fol, uint32_t *__restrict__ nfol,
-                                                   uint32_t *__restrict__ lanes, uint32_t *__restrict__ nlanes,
                                                    const float4 *__restrict__ aos) {
   __shared__ uint32_t fbuf[kWaves][kFolBuf];
   const uint32_t wv = threadIdx.x >> 6;
   uint32_t nf = 0;  // staged follow requests of this wave (uniform)
-  const uint32_t P = __builtin_amdgcn_readfirstlane(*total);
+  const uint32_t D = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(*total >> 32));  // dense chunks
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t nchunks = (P + 63u) / 64u;
   const uint32_t W = gridDim.x * kWaves;
 #if BZR_NEWTON_XCD
   uint32_t q = xcd_contiguous(blockIdx.x, gridDim.x) * kWaves + (threadIdx.x >> 6);
 #else
   uint32_t q = blockIdx.x * kWaves + (threadIdx.x >> 6);
 #endif
-  uint2 pr = make_uint2(0u, 0u);
-  if (q < nchunks && q * 64u + lane < P) pr = pairs[q * 64u + lane];
-  for (; q < nchunks; q += W) {
+  q = __builtin_amdgcn_readfirstlane(q);
+  uint2 pr = make_uint2(kNoPair, 0u);
+  if (q < D) pr = pairs[q * 64u + lane];
+  for (; q < D; q += W) {
     const uint32_t p = q * 64u + lane;
-    bool todo = p < P;
-    const uint32_t ray = pr.x, b = pr.y;
+    const bool todo = pr.x != kNoPair;
+    const uint32_t ray = pr.x & kRayMask, j = pr.x >> 26;
+    const uint32_t b = __builtin_amdgcn_readfirstlane(pr.y);  // the chunk's patch (lane 0 is a real pair)
     f3 s = mk(0.0f, 0.0f, 0.0f), d = s;
     if (todo) load_pair_ray(aos, rays, ld, off, ray, s, d);  // pairs of one patch: mostly neighbouring rays
-    const uint32_t qn = q + W, pn = qn * 64u + lane;  // prefetch the next chunk's pair records
-    if (qn < nchunks && pn < P) pr = pairs[pn];
+    const uint32_t qn = q + W;  // prefetch the next chunk's pair records
+    if (qn < D) pr = pairs[qn * 64u + lane];
     bool is_fol = false;
-    uint32_t fol_entry = 0;
-    // a chunk spanning many small buckets would take one pass per patch here: hand it to k_newton_lane
-    const uint32_t bprev = __shfl_up(b, 1u, 64);
-    const uint32_t distinct = (uint32_t)__popcll(__ballot(todo && (lane == 0u || b != bprev)));
-    if (distinct > kLaneThreshold) {
-      if (lane == 0u) lanes[atomicAdd(nlanes, 1u)] = q;
-      todo = false;
-    }
-    for (;;) {
-      const unsigned long long mask = __ballot(todo);
-      if (mask == 0ull) break;
-      // the next patch of this chunk, wave-uniform: its record is fetched with scalar loads
-      const uint32_t b0 = __builtin_amdgcn_readlane(b, __builtin_ctzll(mask));
-      // formed before the branch: inside it the compiler would substitute the per-lane b for b0
-      const auto pa = uniform_patch(full, b0);
-      if (todo && b == b0) {
-        todo = false;
-        // every pair passed this patch's planar gate in k_traverse (same arithmetic, same record values)
-        const Hit h = patch_intersect<BZR_NEWTON_GATED != 0, kFast>(pa, s, d, false);
-        if (h.what == kIntersect) record(slot, cap, p, h, b0, &key[ray]);
-        is_fol = h.what <= kFollow2;
-        fol_entry = p | (h.what << 30);
-      }
+    const auto pa = uniform_patch(full, b);
+    if (todo) {
+      // every pair passed this patch's planar gate in k_traverse (same arithmetic, same record values)
+      const Hit h = patch_intersect<BZR_NEWTON_GATED != 0, kFast>(pa, s, d, false);
+      if (h.what == kIntersect) record(slot, n, ray, j, b, h, b, &key[ray]);
+      is_fol = h.what <= kFollow2;
+      if (is_fol) reinterpret_cast<uint32_t *>(pairs)[2u * p + 1u] = b | (h.what << 30);  // the side, for k_resolve
     }
     // follow requests: staged in this wave's LDS buffer, published with one atomic per flush
     const unsigned long long fm = __ballot(is_fol);
     if (fm) {
-      if (is_fol) fbuf[wv][nf + lanes_below(fm)] = fol_entry;
+      if (is_fol) fbuf[wv][nf + lanes_below(fm)] = p;
       nf += (uint32_t)__popcll(fm);
       if (nf > kFolBuf - 64u) flush_follow(fbuf[wv], nf, fol, nfol, lane);
     }
@@ -1297,41 +1330,40 @@ __global__ __launch_bounds__(kBlock) BZR_NEWTON_ATTR void k_newton(const float *
   if (nf) flush_follow(fbuf[wv], nf, fol, nfol, lane);
 }
 
-// The chunks k_newton handed over (more than kLaneThreshold distinct patches): every lane runs its own
-// pair with its own patch record in VGPRs, so a fragmented chunk costs one pass instead of one per patch.
+// The sparse region (buckets' remainders below BZR_DENSE_MIN pairs): every lane runs its own pair with its
+// own patch record, so a chunk of many small buckets costs one pass instead of one per patch.
 template <bool kFast>
-__global__ __launch_bounds__(kBlock) void k_newton_lane(const float *__restrict__ full, const uint32_t *__restrict__ total,
-                                                        const uint2 *__restrict__ pairs, const float *__restrict__ rays,
-                                                        uint32_t ld, uint32_t off, float *__restrict__ slot,
-                                                        uint32_t cap, unsigned long long *__restrict__ key,
+__global__ __launch_bounds__(kBlock) void k_newton_lane(const float *__restrict__ full,
+                                                        const unsigned long long *__restrict__ total,
+                                                        uint2 *__restrict__ pairs, const float *__restrict__ rays,
+                                                        uint32_t ld, uint32_t off, uint32_t n, float *__restrict__ slot,
+                                                        unsigned long long *__restrict__ key,
                                                         uint32_t *__restrict__ fol, uint32_t *__restrict__ nfol,
-                                                        const uint32_t *__restrict__ lanes,
-                                                        const uint32_t *__restrict__ nlanes,
                                                         const float4 *__restrict__ aos) {
-  const uint32_t P = __builtin_amdgcn_readfirstlane(*total);
-  const uint32_t C = __builtin_amdgcn_readfirstlane(*nlanes);
+  const unsigned long long tot = *total;
+  const uint32_t base = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(tot >> 32)) * 64u;
+  const uint32_t S = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(tot));
   const uint32_t lane = threadIdx.x & 63u;
-  for (uint32_t c = blockIdx.x * kWaves + (threadIdx.x >> 6); c < C; c += gridDim.x * kWaves) {
-    const uint32_t p = lanes[c] * 64u + lane;
+  for (uint32_t c = blockIdx.x * kWaves + (threadIdx.x >> 6); c * 64u < S; c += gridDim.x * kWaves) {
+    const uint32_t p = base + c * 64u + lane;
     bool is_fol = false;
-    uint32_t fol_entry = 0;
-    if (p < P) {
+    if (c * 64u + lane < S) {
       const uint2 pr = pairs[p];
-      const uint32_t b = pr.y;
+      const uint32_t ray = pr.x & kRayMask, j = pr.x >> 26, b = pr.y;
       f3 s, d;
-      load_pair_ray(aos, rays, ld, off, pr.x, s, d);
+      load_pair_ray(aos, rays, ld, off, ray, s, d);
       const Patch pa = load_patch(full + (size_t)rec::kWords * b);
       const Hit h = patch_intersect<BZR_NEWTON_GATED != 0, kFast>(pa, s, d, false);
-      if (h.what == kIntersect) record(slot, cap, p, h, b, &key[pr.x]);
+      if (h.what == kIntersect) record(slot, n, ray, j, b, h, b, &key[ray]);
       is_fol = h.what <= kFollow2;
-      fol_entry = p | (h.what << 30);
+      if (is_fol) reinterpret_cast<uint32_t *>(pairs)[2u * p + 1u] = b | (h.what << 30);
     }
     const unsigned long long fm = __ballot(is_fol);
     if (fm) {
-      uint32_t base = 0;
-      if (lane == 0u) base = atomicAdd(nfol, (uint32_t)__popcll(fm));
-      base = __builtin_amdgcn_readfirstlane(base);
-      if (is_fol) fol[base + lanes_below(fm)] = fol_entry;
+      uint32_t fb = 0;
+      if (lane == 0u) fb = atomicAdd(nfol, (uint32_t)__popcll(fm));
+      fb = __builtin_amdgcn_readfirstlane(fb);
+      if (is_fol) fol[fb + lanes_below(fm)] = p;
     }
   }
 }
@@ -1353,11 +1385,12 @@ __global__ __launch_bounds__(kBlock) void k_finish(MeshView m, const float *rays
   uint32_t patch = 0xFFFFFFFFu;
   const unsigned long long k = w.key[i];
   if (w.count[i] > kMaxCand) {  // overflow ray: k_resolve left (t order, scanned patch) -- evaluate it again
+    // (in a separate launch over the overflow list instead, k_finish would drop from 112 VGPRs to far fewer:
+    // measured no faster -- an HBM-bound kernel -- and +30 % on cfg2's short frames; r04_ab_finish_split.jsonl)
     if (k != ~0ull) h = evaluate_patch<kFast>(m, static_cast<uint32_t>(k), s, d, patch);
   } else if (k != ~0ull) {
-    const uint32_t p = static_cast<uint32_t>(k);
-
-    const float4 *r = reinterpret_cast<const float4 *>(w.slot) + (size_t)3 * p;  // AoS: 48 bytes per pair
+    const size_t sl = (size_t)(static_cast<uint32_t>(k) & 63u) * n + i;  // the winner's list slot (record())
+    const float4 *r = reinterpret_cast<const float4 *>(w.slot) + 3 * sl;  // AoS: 48 bytes per slot
     const float4 r0 = r[0], r1 = r[1], r2 = r[2];
     h.t = r0.x;
     h.point = mk(r0.y, r0.z, r0.w);
@@ -1393,17 +1426,17 @@ __device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v)
 // one launch per segment saved over separate kernels.
 template <bool kFast>
 __global__ __launch_bounds__(kBlock) void k_resolve(MeshView m, const float *__restrict__ rays, uint32_t ld,
-                                                    uint32_t off, Work w) {
+                                                    uint32_t off, uint32_t n, Work w) {
   const uint32_t F = __builtin_amdgcn_readfirstlane(w.ctr[0]);
   for (uint32_t q = blockIdx.x * kBlock + threadIdx.x; q < F; q += gridDim.x * kBlock) {
-    const uint32_t f = w.fol[q], p = f & 0x3FFFFFFFu, what = f >> 30;
-    const uint2 pr = w.pairs[p];
+    const uint2 pr = w.pairs[w.fol[q]];
+    const uint32_t ray = pr.x & kRayMask, j = pr.x >> 26, b = pr.y & ~(3u << 30), what = pr.y >> 30;
     f3 s, d;
-    load_pair_ray(w.aos, rays, ld, off, pr.x, s, d);
-    const uint32_t nbr = __float_as_uint(m.full[(size_t)rec::kWords * pr.y + rec::kNeigh + what]);
+    load_pair_ray(w.aos, rays, ld, off, ray, s, d);
+    const uint32_t nbr = __float_as_uint(m.full[(size_t)rec::kWords * b + rec::kNeigh + what]);
     Patch pa = load_patch(m.full + (size_t)rec::kWords * nbr);
     Hit h = patch_intersect<false, kFast>(pa, s, d, true);
-    if (h.what == kIntersect) record(w.slot, w.cap, p, h, nbr, &w.key[pr.x]);
+    if (h.what == kIntersect) record(w.slot, n, ray, j, b, h, nbr, &w.key[ray]);  // ranks at its candidate
   }
   const uint32_t V = __builtin_amdgcn_readfirstlane(w.ctr[1]);
   const uint32_t S = (m.n + kOvfSlice - 1) / kOvfSlice;
@@ -1435,43 +1468,44 @@ __global__ __launch_bounds__(kBlock) void k_resolve(MeshView m, const float *__r
 __global__ void k_count(Work w, uint32_t nb, unsigned long long *__restrict__ counters) {
   if (threadIdx.x != 0) return;
   counters[BZR_COUNTER_SEGMENTS] += w.ctr[2];
-  counters[BZR_COUNTER_PAIRS] += w.offs[nb];
+  counters[BZR_COUNTER_PAIRS] += w.ctr[3];
   counters[BZR_COUNTER_FOLLOWS] += w.ctr[0];
   counters[BZR_COUNTER_OVERFLOW_RAYS] += w.ctr[1];
-  counters[BZR_COUNTER_LANE_CHUNKS] += w.ctr[3];
+  // k_newton_lane's chunks; Newton passes = dense chunks + those
+  const unsigned long long tot = w.offs[nb];
+  const uint32_t sparse_chunks = (static_cast<uint32_t>(tot) + 63u) / 64u;
+  counters[BZR_COUNTER_LANE_CHUNKS] += sparse_chunks;
+  counters[BZR_COUNTER_NEWTON_ROUNDS] += static_cast<uint32_t>(tot >> 32) + sparse_chunks;
 }
 
-// Exclusive prefix sum of the per-patch histogram in one block (meshes of up to kScanSmall - 1 patches;
-// larger ones use hipCUB): offs[i] = sum of hist[j < i].  It clears each histogram word it has read,
-// which leaves the histogram zero for the next segment (no memset launch).
+// Exclusive prefix sum of bucket_split(hist) in one block (meshes of up to kScanSmall - 1 patches; larger
+// ones use hipCUB over the same values): offs[i] = sum of BucketSplit(hist[j]) over j < i.  (k_place clears
+// the histogram.)
 constexpr uint32_t kScanThreads = 1024, kScanPer = 8, kScanSmall = kScanThreads * kScanPer;
-__global__ __launch_bounds__(kScanThreads) void k_scan_small(uint32_t *__restrict__ hist, uint32_t *__restrict__ offs,
-                                                             uint32_t count) {
-  __shared__ uint32_t wave_total[kScanThreads / 64];
+__global__ __launch_bounds__(kScanThreads) void k_scan_small(const uint32_t *__restrict__ hist,
+                                                             unsigned long long *__restrict__ offs, uint32_t count) {
+  __shared__ unsigned long long wave_total[kScanThreads / 64];
   const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6, base = t * kScanPer;
-  uint32_t v[kScanPer], sum = 0;
+  unsigned long long v[kScanPer], sum = 0;
 #pragma unroll
   for (uint32_t k = 0; k < kScanPer; ++k) {
-    v[k] = base + k < count ? hist[base + k] : 0u;
+    v[k] = base + k < count ? BucketSplit()(hist[base + k]) : 0ull;
     sum += v[k];
   }
-  uint32_t x = sum;  // inclusive scan over the wave
+  unsigned long long x = sum;  // inclusive scan over the wave
 #pragma unroll
   for (uint32_t d = 1; d < 64; d <<= 1) {
-    const uint32_t y = __shfl_up(x, d, 64);
+    const unsigned long long y = __shfl_up(x, d, 64);
     if (lane >= d) x += y;
   }
   if (lane == 63) wave_total[wv] = x;
   __syncthreads();
-  uint32_t before = 0;
+  unsigned long long before = 0;
   for (uint32_t k = 0; k < wv; ++k) before += wave_total[k];
-  uint32_t run = before + x - sum;
+  unsigned long long run = before + x - sum;
 #pragma unroll
   for (uint32_t k = 0; k < kScanPer; ++k) {
-    if (base + k < count) {
-      offs[base + k] = run;
-      hist[base + k] = 0u;
-    }
+    if (base + k < count) offs[base + k] = run;
     run += v[k];
   }
 }
@@ -2306,15 +2340,16 @@ uint32_t resident_blocks(bzr_ctx *ctx, K kernel) {
 }
 
 // Workspace of the culled path for chunks of up to `chunk` rays over meshes of up to `nb` patches.
+using SplitIt = hipcub::TransformInputIterator<unsigned long long, BucketSplit, const uint32_t *>;
 bzr_status ensure_work(bzr_ctx *ctx, uint32_t chunk, uint32_t nb, Work &w) {
   size_t cub_bytes = 0;
   const uint32_t hn = nb;  // histogram slots, one per patch
-  BZR_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, cub_bytes, static_cast<uint32_t *>(nullptr),
-                                           static_cast<uint32_t *>(nullptr), hn + 1, ctx->stream));
+  BZR_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, cub_bytes, SplitIt(static_cast<const uint32_t *>(nullptr), BucketSplit()),
+                                           static_cast<unsigned long long *>(nullptr), hn + 1, ctx->stream));
   const size_t cap = (size_t)kMaxCand * chunk;
-  const size_t bytes = round256(32) + round256((size_t)(hn + 1) * 4) + round256((size_t)(hn + 1) * 4) + 2 * round256(cap * 4) +
+  const size_t bytes = round256(32) + round256((size_t)(hn + 1) * 4) + round256((size_t)(hn + 1) * 8) + 2 * round256(cap * 4) +
                        round256((size_t)chunk * 4) + round256((size_t)chunk * 8) + round256(kSlotWords * cap * 4) +
-                       round256(cap * 8) + round256(cap * 4) + round256((size_t)chunk * 4) + round256((cap / 64 + 1) * 4) +
+                       round256((cap + 64 * ((size_t)nb + 1)) * 8) + round256(cap * 4) + round256((size_t)chunk * 4) +
                        (BZR_STAGED_AOS ? round256((size_t)chunk * 32) : 0) + round256(cub_bytes);
   const size_t had = ctx->work_bytes;
   if (bzr_status s = ensure_buffer(ctx->work, ctx->work_bytes, bytes)) return s;
@@ -2322,16 +2357,15 @@ bzr_status ensure_work(bzr_ctx *ctx, uint32_t chunk, uint32_t nb, Work &w) {
   Staging st{static_cast<char *>(ctx->work)};
   w.ctr = st.take<uint32_t>(8);
   w.hist = st.take<uint32_t>(hn + 1);
-  w.offs = st.take<uint32_t>(hn + 1);
+  w.offs = st.take<unsigned long long>(hn + 1);
   w.cand = st.take<uint32_t>(cap);
   w.rank = st.take<uint32_t>(cap);
   w.count = st.take<uint32_t>(chunk);
   w.key = st.take<unsigned long long>(chunk);
   w.slot = st.take<float>(kSlotWords * cap);
-  w.pairs = st.take<uint2>(cap);
+  w.pairs = st.take<uint2>(cap + 64 * ((size_t)nb + 1));  // dense chunks (< 64 padding slots per patch) + sparse
   w.fol = st.take<uint32_t>(cap);
   w.ovf = st.take<uint32_t>(chunk);
-  w.lanes = st.take<uint32_t>(cap / 64 + 1);
   w.aos = BZR_STAGED_AOS ? st.take<float4>((size_t)2 * chunk) : nullptr;
   w.cub = st.take<char>(cub_bytes ? cub_bytes : 1);
   w.cub_bytes = cub_bytes;
@@ -2339,7 +2373,7 @@ bzr_status ensure_work(bzr_ctx *ctx, uint32_t chunk, uint32_t nb, Work &w) {
   return BZR_OK;
 }
 
-// Rays per chunk of the staged path, whose workspace is ~2.7 KB per ray: at most
+// Rays per chunk of the staged path, whose workspace is ~2.7 KB per ray + 0.5 KB per patch: at most
 // 2^BZR_CHUNK_LOG2 (8M rays, ~23 GB) and at most what a quarter of the device's free memory holds (at the
 // context's first staged call), with the
 // batch split into equal chunks (rounded to whole waves).  Measured on cfg5 (67M rays): 1M-ray chunks
@@ -2349,6 +2383,9 @@ bzr_status ensure_work(bzr_ctx *ctx, uint32_t chunk, uint32_t nb, Work &w) {
 #endif
 constexpr uint32_t kChunk = 1u << BZR_CHUNK_LOG2;
 constexpr size_t kWorkBytesPerRay = (size_t)kMaxCand * (4 + 4 + 48 + 8 + 4) + 16 + (BZR_STAGED_AOS ? 32 : 0);
+static_assert(BZR_CHUNK_LOG2 <= 26, "pair records hold a chunk's ray index in 26 bits");
+static_assert((uint64_t)kMaxCand * kChunk + 64ull * (kStagedPatchLimit + 1) < (1ull << 32), "32-bit pair indices");
+static_assert(kMaxCand <= 64, "winner keys hold a list slot in 6 bits");
 uint32_t chunk_for(bzr_ctx *ctx, uint64_t n) {
   if (!ctx->chunk_cap) {
     size_t free_b = 0, total_b = 0;
@@ -2369,6 +2406,7 @@ bzr_status run_culled(bzr_ctx *ctx, const MeshView &mv, const float *rays, uint3
   const uint32_t nb = mv.n;
   const uint32_t hn = nb;
   const bool small_scan = hn + 1 <= kScanSmall;
+  if (nb >= kStagedPatchLimit) return BZR_ERR_INVALID_ARGUMENT;  // (the fused path takes any mesh)
   if (!(ctx->zero_ctr == w.ctr && ctx->zero_hn >= hn))  // counters + histogram [0, hn] to zero
     BZR_HIP(hipMemsetAsync(w.ctr, 0, reinterpret_cast<char *>(w.hist + hn + 1) - reinterpret_cast<char *>(w.ctr),
                            ctx->stream));
@@ -2380,31 +2418,30 @@ bzr_status run_culled(bzr_ctx *ctx, const MeshView &mv, const float *rays, uint3
     if (small_scan)
       hipLaunchKernelGGL(k_scan_small, dim3(1), dim3(kScanThreads), 0, ctx->stream, w.hist, w.offs, hn + 1);
     else
-      BZR_HIP(hipcub::DeviceScan::ExclusiveSum(w.cub, w.cub_bytes, w.hist, w.offs, hn + 1, ctx->stream));
-    launch(ctx, -1, k_scatter, dim3(grid_for(n)), rays, ld, off, n, w);
+      BZR_HIP(hipcub::DeviceScan::ExclusiveSum(w.cub, w.cub_bytes, SplitIt(w.hist, BucketSplit()), w.offs, hn + 1,
+                                               ctx->stream));
+    launch(ctx, -1, k_place, dim3(grid_for(std::max(n, nb))), n, nb, w,
+           (ctx->counting && ctx->counters) ? w.ctr + 3 : nullptr);
   }
   // persistent grid: the resident capacity of the device, never more than the worst-case chunk count
   const uint32_t gn = std::min<uint32_t>(std::max<uint32_t>((kMaxCand * n + kBlock - 1) / kBlock, 1u),
                                          resident_blocks(ctx, k_newton<kFast>));
-  launch(ctx, BZR_KERNEL_NEWTON, k_newton<kFast>, dim3(gn), mv.full, w.offs + hn, w.pairs, rays, ld, off, w.slot, w.cap, w.key, w.fol,
-         w.ctr, w.lanes, w.ctr + 3, (const float4 *)w.aos);
+  launch(ctx, BZR_KERNEL_NEWTON, k_newton<kFast>, dim3(gn), mv.full, w.offs + hn, w.pairs, rays, ld, off, n, w.slot, w.key,
+         w.fol, w.ctr, (const float4 *)w.aos);
   launch(ctx, BZR_KERNEL_NEWTON_LANE, k_newton_lane<kFast>, dim3(std::min<uint32_t>(std::max<uint32_t>(n / 1024u, 1u), 1024u)),
-         mv.full, w.offs + hn, w.pairs, rays, ld, off, w.slot, w.cap, w.key, w.fol, w.ctr, w.lanes, w.ctr + 3,
-         (const float4 *)w.aos);
+         mv.full, w.offs + hn, w.pairs, rays, ld, off, n, w.slot, w.key, w.fol, w.ctr, (const float4 *)w.aos);
   {  // follow retries + overflow rays (whose keys the Newton stage left untouched: their lists are empty)
     const uint64_t items = (uint64_t)n * ((nb + kOvfSlice - 1) / kOvfSlice);
     const uint32_t grid = std::max(std::min<uint32_t>(grid_for(n / 8 + 1), 1024u),
                                    (uint32_t)std::min<uint64_t>(items, BZR_OVERFLOW_BLOCKS));
-    launch(ctx, BZR_KERNEL_FOLLOW, k_resolve<kFast>, dim3(std::max<uint32_t>(grid, 1u)), mv, rays, ld, off, w);
+    launch(ctx, BZR_KERNEL_FOLLOW, k_resolve<kFast>, dim3(std::max<uint32_t>(grid, 1u)), mv, rays, ld, off, n, w);
   }
   if (ctx->counting && ctx->counters)  // before k_finish, which clears the counters
     hipLaunchKernelGGL(k_count, dim3(1), dim3(64), 0, ctx->stream, w, nb, ctx->counters);
   launch(ctx, BZR_KERNEL_FINISH, k_finish<kMode, kFast>, dim3(grid_for(n)), mv, rays, ld, off, n, w, o);
   BZR_HIP(hipGetLastError());
-  if (small_scan) {
-    ctx->zero_ctr = w.ctr;
-    ctx->zero_hn = hn;
-  }
+  ctx->zero_ctr = w.ctr;  // k_place cleared the histogram, k_finish the counters
+  ctx->zero_hn = hn;
   return BZR_OK;
 }
 
