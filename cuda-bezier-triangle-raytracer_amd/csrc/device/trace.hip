@@ -1247,12 +1247,29 @@ __global__ __launch_bounds__(kBlock) void k_place(uint32_t n, uint32_t nb, Work 
   if (cnt > kMaxCand || cnt == 0) return;
   const unsigned long long tot = w.offs[nb];
   const uint32_t sparse0 = static_cast<uint32_t>(tot >> 32) * 64u;  // the sparse region's first pair
-  for (uint32_t j = 0; j < cnt; ++j) {
-    const uint32_t b = w.cand[(size_t)j * n + t], r = w.rank[(size_t)j * n + t];
-    const unsigned long long o0 = w.offs[b], o1 = w.offs[b + 1];
-    const uint32_t dbase = static_cast<uint32_t>(o0 >> 32), dlen = 64u * (static_cast<uint32_t>(o1 >> 32) - dbase);
-    const uint32_t p = r < dlen ? dbase * 64u + r : sparse0 + static_cast<uint32_t>(o0) + (r - dlen);
-    w.pairs[p] = make_uint2(t | (j << 26), b);
+  // four list slots per round: their loads first, then the offsets, then the stores (two round trips per
+  // round instead of two per slot)
+  for (uint32_t j0 = 0; j0 < cnt; j0 += 4u) {
+    uint32_t b[4], r[4];
+    unsigned long long o0[4], o1[4];
+#pragma unroll
+    for (uint32_t k = 0; k < 4u; ++k) {
+      const uint32_t j = j0 + k < cnt ? j0 + k : j0;
+      b[k] = w.cand[(size_t)j * n + t];
+      r[k] = w.rank[(size_t)j * n + t];
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < 4u; ++k) {
+      o0[k] = w.offs[b[k]];
+      o1[k] = w.offs[b[k] + 1u];
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < 4u; ++k) {
+      if (j0 + k >= cnt) break;
+      const uint32_t dbase = static_cast<uint32_t>(o0[k] >> 32), dlen = 64u * (static_cast<uint32_t>(o1[k] >> 32) - dbase);
+      const uint32_t p = r[k] < dlen ? dbase * 64u + r[k] : sparse0 + static_cast<uint32_t>(o0[k]) + (r[k] - dlen);
+      w.pairs[p] = make_uint2(t | ((j0 + k) << 26), b[k]);
+    }
   }
 }
 

@@ -39,6 +39,11 @@ for s in $STEPS; do
     prof)   step prof 1500 env TAG="${PROF_TAG:-prof}" BENCH="${PROF_BENCH:-}" WORKLOAD="${PROF_WORKLOAD:-}" \
               bash scripts/prof_run.sh ;;
     dropin) step dropin 400 bash scripts/dropin_latency.sh ;;
+    # bench lines of the other configs on both pipelines (bench defaults, 100 timed steps): configs.jsonl
+    configs) for c in cfg5 cfg3 cfg2; do for p in staged fused; do
+               step "configs_${c}_$p" 300 python bench.py --config $c --pipeline $p --steps 100 --cpu-baseline off &&
+               grep -h '^{' "$OUT/configs_${c}_$p.log" >> "$OUT/configs.jsonl"
+             done; done ;;
     ab)     step ab 900 python scripts/ab.py ${AB_ARGS:-} ;;
     ab2)    step ab2 900 python scripts/ab.py ${AB2_ARGS:-} ;;
     ab3)    step ab3 900 python scripts/ab.py ${AB3_ARGS:-} ;;
