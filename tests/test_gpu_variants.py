@@ -7,6 +7,10 @@ joined retry state must stay valid across the switch.  The default 64-entry stac
 bench configs, so only this build exercises that path: fused == staged == brute force (and == the oracle
 on cfg2), bit for bit, with the device counters reporting overflow rays.
 
+dense1 / dense64: libbzr with the staged pair layout's two extremes (-DBZR_DENSE_MIN=1: every bucket's last
+partial chunk padded, no sparse region; =64: no padding, every remainder in the sparse region): staged ==
+brute force (== the oracle on cfg2 and the cfg4 chain) through only the dense or mostly the sparse kernel.
+
 rpl2 / rpl4: libbzr whose fused kernel is k_trace_r (trace_pool.inc): 2 or 4 rays per lane, the Newton passes
 pooled over a wave's 128 / 256 rays (-DBZR_TRACE_RPL); the same checks plus cfg4's two-lens chain and origins
 beyond s_max (the in-order scan inside the pooled kernel), fused == brute force == the oracle.
@@ -73,13 +77,15 @@ for name, mode in (("fused", bzr.PIPELINE_FUSED), ("staged", bzr.PIPELINE_STAGED
     cnt = ctx.counters_report(); ctx.counters(False)
     out[f"cfg5_{name}_equal"] = bool(np.array_equal(got, ref))
     out[f"cfg5_{name}_overflow_rays"] = cnt["overflow_rays"]
+    out[f"cfg5_{name}_lane_chunks"] = cnt["lane_chunks"]
+    out[f"cfg5_{name}_pairs"] = cnt["pairs"]
 if "--more" in sys.argv:
     # cfg4: two lenses, the chain, 256^2 primaries: fused == brute force == the oracle
     l4 = [build_lens(bzr.TriMesh, l).bezier_patches() for l in CONFIGS["cfg4"].lenses]
     d4 = [bzr.DeviceMesh(ctx, p) for p in l4]
     r4 = grid_rays(CONFIGS["cfg4"], side=256)
     w4 = orc.trace_chain(l4, [1.3, 1.3], r4)
-    for name, mode in (("fused", bzr.PIPELINE_FUSED), ("brute", bzr.ACCEL_NONE)):
+    for name, mode in (("fused", bzr.PIPELINE_FUSED), ("staged", bzr.PIPELINE_STAGED), ("brute", bzr.ACCEL_NONE)):
         g4 = bzr.trace_chain(ctx, d4, [1.3, 1.3], r4, mode=mode)
         out[f"cfg4_{name}_equal"] = all(np.array_equal(bits(g), bits(w)) for g, w in zip(g4, w4))
     # origins beyond s_max mixed into the waves (the in-order scan): robot.stl, 25 % far
@@ -161,3 +167,25 @@ def test_pooled_passes_are_exact(variant):
             assert v, (k, out)
     assert out["cfg2_fused_overflow_rays"] == 0 and out["cfg5_fused_overflow_rays"] == 0
     assert out["far_overflow_rays"] == out["far_count"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", ["dense1", "dense64"])
+def test_staged_pair_layout_extremes_are_exact(variant):
+    """The staged path with every remainder padded (dense1) or none (dense64): bit-identical to the brute-force
+    scan and the oracle; dense1 runs no sparse chunk, dense64 runs every bucket remainder per lane."""
+    lib = PKG / "lib" / variant / "libbzr.so"
+    if not lib.exists():
+        pytest.fail(f"{lib} missing: build() makes the `variants` target")
+    env = dict(os.environ, BZR_LIBRARY=str(lib))
+    res = subprocess.run([sys.executable, "-c", WORKER, str(PKG), str(REPO), "--more"], env=env,
+                         capture_output=True, text=True, timeout=110)
+    assert res.returncode == 0, res.stderr[-2000:]
+    out = json.loads(res.stdout.strip().splitlines()[-1])
+    for k, v in out.items():
+        if k.endswith("_equal"):
+            assert v, (k, out)
+    if variant == "dense1":
+        assert out["cfg5_staged_lane_chunks"] == 0, out
+    else:
+        assert out["cfg5_staged_lane_chunks"] > 0, out
