@@ -22,6 +22,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <climits>
 
 #include <cstdio>
 #include <cstring>
@@ -594,9 +595,7 @@ typedef __attribute__((address_space(4))) const u32x8 cu32x8;
 //      [L - B|p~| - C(|s|+|p~|), H + ...] at p~ = s + d (num x rcp(cs)) -- ~3 % of cfg5's pairs pass.
 // Only then the exact gate (the division and fl(M p)), so the always list costs ~25 VALU per pair
 // instead of ~50.  Same candidates as the gate alone.
-__device__ __forceinline__ bool always_gate(const float4 *always, uint32_t k, bool act, f3 s, f3 d, uint32_t &patch) {
-  const u32x16 r = *((const cu32x16 *)(uintptr_t)(always + (size_t)kAlwaysQuads * k));
-  const u32x8 wq = *((const cu32x8 *)(uintptr_t)(always + (size_t)kAlwaysQuads * k + 4));
+__device__ __forceinline__ bool always_gate_rec(const u32x16 &r, const u32x8 &wq, bool act, f3 s, f3 d, uint32_t &patch) {
   patch = r[15];
   const float4 q0 = leaf_q(r, 0);
   const f3 n = mk(q0.x, q0.y, q0.z);
@@ -613,6 +612,11 @@ __device__ __forceinline__ bool always_gate(const float4 *always, uint32_t k, bo
   keep &= !(w > __uint_as_float(wq[4]) + slack) & !(w < __uint_as_float(wq[3]) - slack);
   if (!__any(keep)) return false;
   return keep & planar_gate(q0, leaf_q(r, 1), leaf_q(r, 2), leaf_q(r, 3), s, d);
+}
+__device__ __forceinline__ bool always_gate(const float4 *always, uint32_t k, bool act, f3 s, f3 d, uint32_t &patch) {
+  const u32x16 r = *((const cu32x16 *)(uintptr_t)(always + (size_t)kAlwaysQuads * k));
+  const u32x8 wq = *((const cu32x8 *)(uintptr_t)(always + (size_t)kAlwaysQuads * k + 4));
+  return always_gate_rec(r, wq, act, s, d, patch);
 }
 
 // Wave-level pre-test of the always list.  The active rays of a wave form a bundle: origins in the box
@@ -677,14 +681,31 @@ __device__ __forceinline__ void bundle_to_lds(bool act, f3 s, f3 d, float *out, 
   __builtin_amdgcn_wave_barrier();  // the words are read back by every lane of this wave
 }
 // Wave min / max with DPP row shifts and row broadcasts (no LDS round trips): lane 63 ends with the result,
-// read back as a uniform value.  Lanes shifted in from outside a row contribute the identity.
-template <bool kMax>
-__device__ __forceinline__ float wave_reduce_dpp(float v) {
-  const int id = __float_as_int(kMax ? -__builtin_inff() : __builtin_inff());
-#define BZR_DPP_STEP(ctrl, rows)                                                                        \
-  {                                                                                                    \
-    const float o = __int_as_float(__builtin_amdgcn_update_dpp(id, __float_as_int(v), ctrl, rows, 0xF, false)); \
-    v = kMax ? fmaxf(v, o) : fminf(v, o);                                                              \
+// read back as a uniform value.  Lanes shifted in from outside a row contribute the identity.  The floats are
+// reduced as order-preserving integers (sign-magnitude flipped to two's complement): a float fminf / fmaxf
+// step costs a DPP move, two canonicalising v_max and the min (IEEE mode), an integer step is one
+// v_min_i32 / v_max_i32 with the DPP operand folded in.  NaN lanes contribute the identity (as fminf / fmaxf
+// ignore them); -0 orders below +0 (either is a valid bound).
+__device__ __forceinline__ int float_order(float x) {
+  const int b = __float_as_int(x);
+  return b ^ ((b >> 31) & 0x7FFFFFFF);
+}
+// The 12 bundle reductions in lockstep (step k of all twelve, then step k + 1): each DPP read is then 12
+// instructions behind the write it reads, so no s_nop hazard padding between the steps.  kMaxMask bit i:
+// value i is reduced by max (else min).
+template <uint32_t kMaxMask>
+__device__ __forceinline__ void wave_reduce12_dpp(const float (&x)[12], float (&out)[12]) {
+  int v[12];
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    const int id = ((kMaxMask >> i) & 1u) ? INT_MIN : INT_MAX;
+    v[i] = x[i] == x[i] ? float_order(x[i]) : id;
+  }
+#define BZR_DPP_STEP(ctrl, rows)                                                        \
+  _Pragma("unroll") for (int i = 0; i < 12; ++i) {                                     \
+    const bool mx = (kMaxMask >> i) & 1u;                                              \
+    const int o = __builtin_amdgcn_update_dpp(mx ? INT_MIN : INT_MAX, v[i], ctrl, rows, 0xF, false); \
+    v[i] = mx ? max(v[i], o) : min(v[i], o);                                           \
   }
   BZR_DPP_STEP(0x111, 0xF)  // row_shr:1
   BZR_DPP_STEP(0x112, 0xF)  // row_shr:2
@@ -693,7 +714,11 @@ __device__ __forceinline__ float wave_reduce_dpp(float v) {
   BZR_DPP_STEP(0x142, 0xA)  // row_bcast:15 into rows 1 and 3
   BZR_DPP_STEP(0x143, 0xC)  // row_bcast:31 into rows 2 and 3: lane 63 holds the wave's result
 #undef BZR_DPP_STEP
-  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    const int r = __builtin_amdgcn_readlane(v[i], 63);
+    out[i] = __int_as_float(r ^ ((r >> 31) & 0x7FFFFFFF));  // (the map is its own inverse)
+  }
 }
 // The whole bundle with the 12 reductions side by side in DPP form, written by lane 0: words 0..12 as
 // bundle_to_lds, and for the bundle walk 13..21 -- per axis rl = 1 / Dl', rh = 1 / Dh' and mixed = 1 when
@@ -701,13 +726,11 @@ __device__ __forceinline__ float wave_reduce_dpp(float v) {
 // a wider direction box, so a superset of the rays).
 __device__ __forceinline__ float bundle_setup_dpp(bool act, f3 s, f3 d, float *out, uint32_t lane) {
   const float inf = __builtin_inff();
-  const float r[12] = {
-      wave_reduce_dpp<false>(act ? s.x : inf),  wave_reduce_dpp<false>(act ? s.y : inf),
-      wave_reduce_dpp<false>(act ? s.z : inf),  wave_reduce_dpp<true>(act ? s.x : -inf),
-      wave_reduce_dpp<true>(act ? s.y : -inf),  wave_reduce_dpp<true>(act ? s.z : -inf),
-      wave_reduce_dpp<false>(act ? d.x : inf),  wave_reduce_dpp<false>(act ? d.y : inf),
-      wave_reduce_dpp<false>(act ? d.z : inf),  wave_reduce_dpp<true>(act ? d.x : -inf),
-      wave_reduce_dpp<true>(act ? d.y : -inf),  wave_reduce_dpp<true>(act ? d.z : -inf)};
+  const float x[12] = {act ? s.x : inf,  act ? s.y : inf,  act ? s.z : inf,  act ? s.x : -inf,
+                       act ? s.y : -inf, act ? s.z : -inf, act ? d.x : inf,  act ? d.y : inf,
+                       act ? d.z : inf,  act ? d.x : -inf, act ? d.y : -inf, act ? d.z : -inf};
+  float r[12];
+  wave_reduce12_dpp<0xE38u>(x, r);  // max: values 3, 4, 5, 9, 10, 11
   if (lane == 0u) {
     float m = 0.0f;
 #pragma unroll
@@ -798,12 +821,10 @@ __device__ __forceinline__ void ivdot(f3 n, f3 lo, f3 hi, float &a, float &b) {
 }
 __device__ __forceinline__ float absmax(float lo, float hi) { return fmaxf(fabsf(lo), fabsf(hi)); }
 // false: no ray of the bundle (LDS words bl) can pass always-listed patch k's gate.
-__device__ __forceinline__ bool always_bundle_keep(const float4 *always, uint32_t k, uint32_t n_always, const float *bl) {
-  if (k >= n_always) return false;
+__device__ __forceinline__ bool always_bundle_keep_rec(float4 q0, float4 w0, float4 w1, const float *bl) {
   const float *B = bl;
   if (!(B[12] > 0.0f)) return true;
   constexpr float u = 0x1p-24f;
-  const float4 q0 = always[(size_t)kAlwaysQuads * k];
   const f3 n = mk(q0.x, q0.y, q0.z);
   float csl, csh, nsl, nsh;
   ivdot(n, mk(B[6], B[7], B[8]), mk(B[9], B[10], B[11]), csl, csh);
@@ -824,7 +845,6 @@ __device__ __forceinline__ bool always_bundle_keep(const float4 *always, uint32_
   if (thi <= 0.0f) return false;     // t > 0 for no ray
   tlo = fmaxf(tlo, 0.0f);
   // plane points P = S + D T and the wedge w.P, one axis at a time
-  const float4 w0 = always[(size_t)kAlwaysQuads * k + 4];
   float wlo = 0.0f, whi = 0.0f, pm0 = 0.0f, smax = 0.0f, wabs = 0.0f;
 #pragma unroll
   for (int a = 0; a < 3; ++a) {
@@ -844,9 +864,13 @@ __device__ __forceinline__ bool always_bundle_keep(const float4 *always, uint32_
   const float pmax = pm0 + e;
   wlo -= wabs * e;
   whi += wabs * e;
-  const float4 w1 = always[(size_t)kAlwaysQuads * k + 5];
   const float slack = w1.y * pmax + (w1.z + 64.0f * u) * (smax + pmax);
   return !(wlo > w1.x + slack) & !(whi < w0.w - slack);
+}
+__device__ __forceinline__ bool always_bundle_keep(const float4 *always, uint32_t k, uint32_t n_always, const float *bl) {
+  if (k >= n_always) return false;
+  const float4 *a = always + (size_t)kAlwaysQuads * k;
+  return always_bundle_keep_rec(a[0], a[4], a[5], bl);
 }
 
 // Wave-level pre-test of a tree leaf's planar gate (the bundle walk's queued leaves, one per lane): false
@@ -903,12 +927,36 @@ __device__ __forceinline__ bool bundle_gate_keep(const float *B, float4 q0, floa
   return keep;
 }
 
+// BZR_TRAV_PHASES (diagnostic build, default 0): k_traverse stamps s_memtime at its phase boundaries and, with
+// device counters on, adds each wave's cycles per phase to counter slots (their own counts are small beside
+// them): node_visits <- setup (ray loads, bundle reductions), leaf_fetches <- the queued leaves' per-lane
+// gates, gate_tests <- the walk's batches and leaf pre-tests, overflow_rays <- the per-lane walk, follows <-
+// the always list, segments <- the ranking (variant travph: scripts/ab.py prints them as its counters; the
+// stamps cost ~4 %).
+#ifndef BZR_TRAV_PHASES
+#define BZR_TRAV_PHASES 0
+#endif
+#if BZR_TRAV_PHASES
+#define BZR_PHASE(k)                                          \
+  {                                                           \
+    const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
+    ph_acc[ph_cur] += now_ - ph_t;                            \
+    ph_t = now_;                                              \
+    ph_cur = (k);                                             \
+  }
+#else
+#define BZR_PHASE(k)
+#endif
 // Candidate search.  `alive` (optional): a ray is traced iff alive[off + i] != BZR_RR_NONE.
 // One wave's 64 rays i (lane l of the wave holds ray i); `stk` is the wave's LDS stack.
 __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__restrict__ rays, uint32_t ld,
                                               uint32_t off, const uint32_t *__restrict__ alive, uint32_t n,
                                               const Work &w, unsigned long long *counters, uint32_t i, uint32_t *stk,
                                               float *bl, uint32_t *pend, uint32_t *raw) {
+#if BZR_TRAV_PHASES
+  unsigned long long ph_acc[6] = {0ull, 0ull, 0ull, 0ull, 0ull, 0ull}, ph_t = __builtin_amdgcn_s_memtime();
+  uint32_t ph_cur = 0;
+#endif
   uint32_t c_nodes = 0, c_leaves = 0, c_gates = 0;  // work counters (with counters on; wave-uniform)
   bool active = i < n && (alive == nullptr || alive[off + i] != BZR_RR_NONE);
   f3 s = mk(0.0f, 0.0f, 0.0f), d = s;
@@ -956,6 +1004,7 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
 #endif
   while (bwalk) {
     if (pi < npend) {
+      BZR_PHASE(1)
 #if BZR_TRAV_LEAF_PAIRS
       // two queued leaves per step: both 64-byte records in flight together (one wait for two round trips)
       const bool two = pi + 1u < npend;
@@ -993,6 +1042,7 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
 #endif
       continue;
     }
+    BZR_PHASE(2)
 #if BZR_TRAV_PRETEST
     if (sp == 0 || nraw > 64u) {  // the queued leaves' wave-level gate pre-test: the survivors go to pend
       if (nraw == 0u) break;
@@ -1054,6 +1104,7 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
     if (counters) c_nodes += k;
   }
 #endif
+  BZR_PHASE(3)
   while (next != 0xFFFFFFFFu || sp > 0) {  // the per-lane walk
     const uint32_t node = next != 0xFFFFFFFFu ? next : __builtin_amdgcn_readfirstlane(stk[--sp]);
     next = 0xFFFFFFFFu;
@@ -1090,6 +1141,7 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
     }
   }
   // the always list (patches without a proven gate region, bvh.cpp): gate-tested for every active ray
+  BZR_PHASE(4)
   if (m.n_always && __any(active)) {
 #if BZR_TRAV_BUNDLE
     if (!walk)  // (the bundle walk built it already)
@@ -1109,6 +1161,7 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
         }
       }
     }
+
   }
   if (counters) {  // rays traced (one atomic per wave: on one address, so only with counters on)
     const unsigned long long traced = __ballot(i < n && (alive == nullptr || alive[off + i] != BZR_RR_NONE));
@@ -1117,7 +1170,7 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
     const uint32_t lane = threadIdx.x & 63u, rep = (i >> 6) % kCounterReplicas;
     const uint32_t v = lane == 0u ? c_nodes : (lane == 1u ? c_leaves : c_gates);
     const uint32_t which = lane == 0u ? BZR_COUNTER_NODE_VISITS : (lane == 1u ? BZR_COUNTER_LEAF_FETCHES : BZR_COUNTER_GATE_TESTS);
-    if (lane < 3u && v) atomicAdd(&counters[(size_t)rep * BZR_COUNTER_COUNT + which], (unsigned long long)v);
+    if (!BZR_TRAV_PHASES && lane < 3u && v) atomicAdd(&counters[(size_t)rep * BZR_COUNTER_COUNT + which], (unsigned long long)v);
   }
   if (i >= n) return;
   w.count[i] = cnt;
@@ -1128,6 +1181,7 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
   // each group's first lane adds the group size -- all groups in one atomic instruction -- and the
   // lanes take their rank from the returned base.
   const uint32_t lane = threadIdx.x & 63u;
+  BZR_PHASE(5)
   const uint32_t listed = cnt <= kMaxCand ? cnt : 0u;
   // Four list slots per round: their candidate loads first, then the grouping, then all four rounds'
   // returning atomics in flight together (one wait instead of four: vmcnt retires in issue order).
@@ -1166,6 +1220,22 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
       if (j0 + k < listed) w.rank[(size_t)(j0 + k) * n + i] = bs + below[k];
     }
   }
+#if BZR_TRAV_PHASES
+  BZR_PHASE(0)
+  if (counters && lane < 6u) {
+    const uint32_t id[6] = {BZR_COUNTER_NODE_VISITS, BZR_COUNTER_LEAF_FETCHES, BZR_COUNTER_GATE_TESTS,
+                            BZR_COUNTER_OVERFLOW_RAYS, BZR_COUNTER_FOLLOWS, BZR_COUNTER_SEGMENTS};
+    unsigned long long v = 0ull;
+    uint32_t which = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 6u; ++k)
+      if (lane == k) {
+        v = ph_acc[k];
+        which = id[k];
+      }
+    atomicAdd(&counters[(size_t)((i >> 6) % kCounterReplicas) * BZR_COUNTER_COUNT + which], v);
+  }
+#endif
 }
 
 // Candidate search, one 64-ray wave per 64 consecutive rays.
