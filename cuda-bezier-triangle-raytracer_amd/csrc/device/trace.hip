@@ -90,7 +90,7 @@ constexpr uint32_t kMaxLenses = 8;
 #define BZR_MAX_CAND 40
 #endif
 constexpr uint32_t kMaxCand = BZR_MAX_CAND;  // candidate list length per ray and segment
-constexpr uint32_t kOverflow = 0xFFFFu;  // count value: resolve with the full scan
+constexpr uint32_t kOverflow = 0x8000u;  // count flag: resolve with the full scan (the low bits keep the listed count)
 // Traversal stack entries per wave (LDS).  BZR_STACK (A/B and test knob): a tiny stack makes waves run out
 // mid-walk, which sends the affected lanes to the in-order full scan (tests/test_gpu_variants.py).
 #ifndef BZR_STACK
@@ -500,7 +500,7 @@ struct Work {
   unsigned long long *offs;  // [nb + 1] exclusive prefix of bucket_split(hist); offs[nb] = the totals
   uint32_t *cand;    // [kMaxCand][n]
   uint32_t *rank;    // [kMaxCand][n]
-  uint32_t *count;   // [n]
+  uint32_t *count;   // [n] list length, | kOverflow: the full scan
   unsigned long long *key;  // [n]
   float *slot;       // [kMaxCand][n] x kSlotWords: the hit of ray i's list slot j at j * n + i (AoS, 48 bytes)
   uint2 *pairs;      // [cap + 64 (nb + 1)] pair records (ray | j << 26, patch): dense chunks, then the sparse
@@ -947,6 +947,16 @@ __device__ __forceinline__ bool bundle_gate_keep(const float *B, float4 q0, floa
 #else
 #define BZR_PHASE(k)
 #endif
+// The lanes whose gate of patch b passed list it as their next candidate (while the list has room; a lane
+// past kMaxCand overflows to the full scan).  (Counting the listing lanes into b's histogram word right here --
+// b is wave-uniform, so one atomic without return per wave -- and ranking the pairs in k_place instead of
+// after the walk: k_traverse -1.6 % on cfg5 and -9 % on cfg3, but k_place's grouped ranking atomics cost more
+// than that, cfg3 frames +7.6 %; profiles/r04_ab_rank_late.jsonl.)
+__device__ __forceinline__ void list_candidate(bool pass, uint32_t b, const Work &w, uint32_t n, uint32_t i,
+                                               uint32_t &cnt) {
+  if (pass && cnt < kMaxCand) w.cand[(size_t)cnt * n + i] = b;
+  if (pass) cnt = cnt < kMaxCand ? cnt + 1 : (cnt | kOverflow);
+}
 // Candidate search.  `alive` (optional): a ray is traced iff alive[off + i] != BZR_RR_NONE.
 // One wave's 64 rays i (lane l of the wave holds ray i); `stk` is the wave's LDS stack.
 __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__restrict__ rays, uint32_t ld,
@@ -970,7 +980,7 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
   uint32_t cnt = 0;
   // gate-region boxes hold for ray origins within s_max (bvh.cpp); farther rays take the full scan
   if (active && !(fmaxf(fmaxf(fabsf(s.x), fabsf(s.y)), fabsf(s.z)) <= m.s_max)) {
-    cnt = kOverflow;
+    cnt |= kOverflow;
     active = false;
   }
   // tree tier, wave-uniform: the near tree's tighter boxes hold when every active ray starts within s_near
@@ -1019,14 +1029,11 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
         c_leaves += two ? 2u : 1u;
         c_gates += (two ? 2u : 1u) * (uint32_t)__popcll(__ballot(active));
       }
-      if (active & planar_gate(leaf_q(r0, 0), leaf_q(r0, 1), leaf_q(r0, 2), leaf_q(r0, 3), s, d)) {
-        if (cnt < kMaxCand) w.cand[(size_t)cnt * n + i] = r0[15];
-        cnt = cnt < kMaxCand ? cnt + 1 : kOverflow;
-      }
-      if (two && (active & planar_gate(leaf_q(r1, 0), leaf_q(r1, 1), leaf_q(r1, 2), leaf_q(r1, 3), s, d))) {
-        if (cnt < kMaxCand) w.cand[(size_t)cnt * n + i] = r1[15];
-        cnt = cnt < kMaxCand ? cnt + 1 : kOverflow;
-      }
+      list_candidate(active & planar_gate(leaf_q(r0, 0), leaf_q(r0, 1), leaf_q(r0, 2), leaf_q(r0, 3), s, d), r0[15], w,
+                     n, i, cnt);
+      if (two)
+        list_candidate(active & planar_gate(leaf_q(r1, 0), leaf_q(r1, 1), leaf_q(r1, 2), leaf_q(r1, 3), s, d), r1[15],
+                       w, n, i, cnt);
 #else
       const uint32_t slot = __builtin_amdgcn_readfirstlane(pend[pi]);
       ++pi;
@@ -1035,10 +1042,8 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
         ++c_leaves;
         c_gates += (uint32_t)__popcll(__ballot(active));
       }
-      if (active & planar_gate(leaf_q(r, 0), leaf_q(r, 1), leaf_q(r, 2), leaf_q(r, 3), s, d)) {
-        if (cnt < kMaxCand) w.cand[(size_t)cnt * n + i] = r[15];
-        cnt = cnt < kMaxCand ? cnt + 1 : kOverflow;
-      }
+      list_candidate(active & planar_gate(leaf_q(r, 0), leaf_q(r, 1), leaf_q(r, 2), leaf_q(r, 3), s, d), r[15], w, n,
+                     i, cnt);
 #endif
       continue;
     }
@@ -1092,7 +1097,7 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
           if ((threadIdx.x & 63u) == 0u) stk[sp] = ch[c];
           ++sp;
         } else if ((hm >> (threadIdx.x & 63u)) & 1ull) {
-          cnt = kOverflow;  // stack exhausted: full scan
+          cnt |= kOverflow;  // stack exhausted: full scan
         }
       }
       continue;
@@ -1100,7 +1105,7 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
     bool full;
     uint32_t k;
     qn += bundle_batch<kStack>(kids, stk, sp, qbuf, bl, threadIdx.x & 63u, full, k, qn);
-    if (full && active) cnt = kOverflow;  // stack exhausted: every active lane takes the full scan
+    if (full && active) cnt |= kOverflow;  // stack exhausted: every active lane takes the full scan
     if (counters) c_nodes += k;
   }
 #endif
@@ -1126,14 +1131,11 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
           ++c_leaves;
           c_gates += (uint32_t)__popcll(hm);
         }
-        if (hit[c] & planar_gate(q0, q1, q2, q3, s, d)) {
-          if (cnt < kMaxCand) w.cand[(size_t)cnt * n + i] = r[15];
-          cnt = cnt < kMaxCand ? cnt + 1 : kOverflow;
-        }
+        list_candidate(hit[c] & planar_gate(q0, q1, q2, q3, s, d), r[15], w, n, i, cnt);
       } else {
         if (next != 0xFFFFFFFFu) {
           if (sp < kStack) stk[sp++] = next;
-          else if ((next_hm >> (threadIdx.x & 63u)) & 1ull) cnt = kOverflow;  // stack exhausted: full scan
+          else if ((next_hm >> (threadIdx.x & 63u)) & 1ull) cnt |= kOverflow;  // stack exhausted: full scan
         }
         next = ch[c];
         next_hm = hm;
@@ -1155,10 +1157,8 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
           ++c_leaves;
           c_gates += (uint32_t)__popcll(__ballot(active));
         }
-        if (always_gate(m.always, ab * 64u + __builtin_ctzll(am), active, s, d, b)) {
-          if (cnt < kMaxCand) w.cand[(size_t)cnt * n + i] = b;
-          cnt = cnt < kMaxCand ? cnt + 1 : kOverflow;
-        }
+        const bool pass = always_gate(m.always, ab * 64u + __builtin_ctzll(am), active, s, d, b);
+        list_candidate(pass, b, w, n, i, cnt);
       }
     }
 
@@ -1295,9 +1295,8 @@ struct BucketSplit {
 // 64 dense_base(b) + r while r < 64 dense_chunks(b), else sparse pair r - 64 dense_chunks(b) of the bucket.
 __global__ __launch_bounds__(kBlock) void k_place(uint32_t n, uint32_t nb, Work w, uint32_t *__restrict__ pair_count) {
   const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
-  uint32_t c = 0;
   if (t < nb) {
-    c = w.hist[t];
+    const uint32_t c = w.hist[t];
     if (c) {
       w.hist[t] = 0u;
       if ((c & 63u) >= kDenseMin) {
@@ -1306,27 +1305,25 @@ __global__ __launch_bounds__(kBlock) void k_place(uint32_t n, uint32_t nb, Work 
       }
     }
   }
-  if (pair_count) {  // the wave's listed pairs (bzr_ctx_counters "pairs")
-    uint32_t sum = c;
+  const uint32_t cw = t < n ? w.count[t] : 0u;
+  const uint32_t cnt = cw > kMaxCand ? 0u : cw;  // (an overflow ray's list is not ranked: the full scan takes it)
+  if (pair_count) {  // the wave's listed pairs (bzr_ctx_counters "pairs": the pairs the Newton stage runs)
+    uint32_t sum = cnt;
 #pragma unroll
     for (int k = 32; k >= 1; k >>= 1) sum += __shfl_xor(sum, k, 64);
     if ((threadIdx.x & 63u) == 0u && sum) atomicAdd(pair_count, sum);
   }
-  if (t >= n) return;
-  const uint32_t cnt = w.count[t];
-  if (cnt > kMaxCand || cnt == 0) return;
   const unsigned long long tot = w.offs[nb];
   const uint32_t sparse0 = static_cast<uint32_t>(tot >> 32) * 64u;  // the sparse region's first pair
-  // four list slots per round: their loads first, then the offsets, then the stores (two round trips per
-  // round instead of two per slot)
-  for (uint32_t j0 = 0; j0 < cnt; j0 += 4u) {
+  // four list slots per round: their loads first, then the offsets, then the stores
+  for (uint32_t j0 = 0; __any(j0 < cnt); j0 += 4u) {
     uint32_t b[4], r[4];
     unsigned long long o0[4], o1[4];
 #pragma unroll
     for (uint32_t k = 0; k < 4u; ++k) {
-      const uint32_t j = j0 + k < cnt ? j0 + k : j0;
-      b[k] = w.cand[(size_t)j * n + t];
-      r[k] = w.rank[(size_t)j * n + t];
+      const uint32_t j = j0 + k < cnt ? j0 + k : 0u;
+      b[k] = cnt ? w.cand[(size_t)j * n + t] : 0u;
+      r[k] = cnt ? w.rank[(size_t)j * n + t] : 0u;
     }
 #pragma unroll
     for (uint32_t k = 0; k < 4u; ++k) {
@@ -1434,8 +1431,8 @@ __global__ __launch_bounds__(kBlock) void k_newton_lane(const float *__restrict_
   for (uint32_t c = blockIdx.x * kWaves + (threadIdx.x >> 6); c * 64u < S; c += gridDim.x * kWaves) {
     const uint32_t p = base + c * 64u + lane;
     bool is_fol = false;
-    if (c * 64u + lane < S) {
-      const uint2 pr = pairs[p];
+    const uint2 pr = c * 64u + lane < S ? pairs[p] : make_uint2(kNoPair, 0u);
+    if (pr.x != kNoPair) {
       const uint32_t ray = pr.x & kRayMask, j = pr.x >> 26, b = pr.y;
       f3 s, d;
       load_pair_ray(aos, rays, ld, off, ray, s, d);
