@@ -72,6 +72,8 @@ struct bzr_mesh {
   bzr_host::Bvh4ObbNode *obb_near;
   float4 *kids;      // the far tree's children AoS (2 float4 per child: lo.xyz ref, hi.xyz 0): the bundle walk's
   float4 *kids_near; // per-lane child records (kids_of), and the near tree's
+  float4 *wide;      // two levels per node for k_traverse's bundle walk (BZR_TRAV_WIDE, wide_of): node i's 16
+  float4 *wide_near; // grandchild slots, 2 float4 each as in kids
   float4 *always;   // 8 float4 per always-tested patch (bvh.hpp Bvh::always): planar record with the patch index
                     // in its last word, then the wedge pre-test (always_wedge: w.xyz L H B C 0) and 8 pad words
   uint32_t n_always;
@@ -162,6 +164,15 @@ constexpr int kTravBlock = BZR_TRAV_BLOCK;
 #ifndef BZR_TRAV_LEAF_PAIRS
 #define BZR_TRAV_LEAF_PAIRS 1
 #endif
+// BZR_TRAV_WIDE (default 1): k_traverse's bundle walk takes two tree levels per batch over 16-slot records
+// (bzr_mesh wide / wide_near: each node's grandchildren), 4 nodes per batch instead of 16 nodes' children.
+#ifndef BZR_TRAV_WIDE
+#define BZR_TRAV_WIDE 1
+#endif
+// BZR_TRACE_WIDE (with BZR_TRACE_BUNDLE): k_trace's bundle walk over the same two-level records.
+#ifndef BZR_TRACE_WIDE
+#define BZR_TRACE_WIDE 0
+#endif
 // BZR_TRAV_BUNDLE (default 1): k_traverse walks with the wave-bundle test in batches (traverse_rays):
 // cfg5 8192^2 staged k_traverse 6.61 -> 5.07 ms per frame, cfg3 0.283 -> 0.235, cfg2 0.134 -> 0.143
 // (profiles/r03s2_ab_bundle_walk.jsonl).
@@ -216,6 +227,8 @@ struct MeshView {
   const float4 *__restrict__ always;  // patches without a proven gate region: gate-tested by every wave-segment
   const float4 *__restrict__ kids;       // AoS child records of nodes / nodes_near (bzr_mesh)
   const float4 *__restrict__ kids_near;
+  const float4 *__restrict__ wide;       // 16 grandchild records per node (BZR_TRAV_WIDE)
+  const float4 *__restrict__ wide_near;
   uint32_t n_always;
   uint32_t n;
   float s_max;
@@ -782,23 +795,27 @@ __device__ __forceinline__ bool bundle_box(const float *B, float4 lo, float4 hi)
 // taking node q's child c from the AoS child records `kids`.  Hit inner children are pushed, hit leaf slots
 // written to `pend` (returns how many).  Returns with `full` set when the stack could not take every hit
 // child (those subtrees are dropped: the caller sends its active lanes to the full scan).
-template <int kCap>
+// kSlots = 16: the same over the two-level records `wide` (4 nodes per batch, lane 16 q + s taking slot s of
+// node q), so a batch descends two levels of the tree.
+template <int kCap, uint32_t kSlots = 4>
 __device__ __forceinline__ uint32_t bundle_batch(const float4 *kids, uint32_t *stk, int &sp, uint32_t *pend,
                                                  const float *B, uint32_t lane, bool &full, uint32_t &knodes,
                                                  uint32_t base = 0u) {
   // (the lane index laundered: lane-derived addresses hoisted out of the walk stayed live across the Newton
   // passes of k_trace and cost it a wave of occupancy)
   asm volatile("" : "+v"(lane));
-  const uint32_t q = lane >> 2, c = lane & 3u;
-  // at most (kCap - sp) / 3 nodes (at least one), so their <= 4 children each fit: the stack overflows only
-  // from a nearly full stack (a wide bundle; the walk choice sends those to the per-lane walk)
-  const int room = (kCap - sp) / 3, avail = sp < 16 ? sp : 16;
+  constexpr uint32_t kShift = kSlots == 16u ? 4u : 2u;
+  constexpr int kNodes = 64 / (int)kSlots;
+  const uint32_t q = lane >> kShift, c = lane & (kSlots - 1u);
+  // at most (kCap - sp) / (kSlots - 1) nodes (at least one), so their <= kSlots children each fit: the stack
+  // overflows only from a nearly full stack (a wide bundle; the walk choice sends those to the per-lane walk)
+  const int room = (kCap - sp) / (int)(kSlots - 1u), avail = sp < kNodes ? sp : kNodes;
   const uint32_t kmax = (uint32_t)(avail < room ? avail : (room > 1 ? room : 1));
   const uint32_t nd = q < kmax ? stk[sp - 1 - (int)q] : 0u;
   const unsigned long long ob = __ballot(c == 0u && q < kmax && (nd & bzr_host::kObbFlag));
-  const uint32_t k = ob ? (uint32_t)__builtin_ctzll(ob) >> 2 : kmax;
+  const uint32_t k = ob ? (uint32_t)__builtin_ctzll(ob) >> kShift : kmax;
   const bool slot = q < k;
-  const float4 *kp = kids + ((size_t)(slot ? nd : 0u) * 4u + c) * 2u;
+  const float4 *kp = kids + ((size_t)(slot ? nd : 0u) * kSlots + c) * 2u;
   const float4 lo = kp[0], hi = kp[1];
   const uint32_t ref = __float_as_uint(lo.w);
   const bool hit = slot && ref != bzr_host::kEmptyChild && bundle_box(B, lo, hi);
@@ -1008,6 +1025,10 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
     bwalk = true;
   }
   const float4 *kids = near_tier ? m.kids_near : m.kids;
+#if BZR_TRAV_WIDE
+  const float4 *wide = near_tier ? m.wide_near : m.wide;
+  (void)kids;
+#endif
   uint32_t npend = 0, pi = 0;  // leaves queued in pend, next to gate-test (uniform)
 #if BZR_TRAV_PRETEST
   uint32_t nraw = 0;  // leaves queued in raw, not yet pre-tested
@@ -1104,7 +1125,11 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
     }
     bool full;
     uint32_t k;
+#if BZR_TRAV_WIDE
+    qn += bundle_batch<kStack, 16>(wide, stk, sp, qbuf, bl, threadIdx.x & 63u, full, k, qn);
+#else
     qn += bundle_batch<kStack>(kids, stk, sp, qbuf, bl, threadIdx.x & 63u, full, k, qn);
+#endif
     if (full && active) cnt |= kOverflow;  // stack exhausted: every active lane takes the full scan
     if (counters) c_nodes += k;
   }
@@ -1879,7 +1904,11 @@ __device__ __forceinline__ void trace_segment(const MeshView &m, f3 s, f3 d, boo
       }
       bool full;
       uint32_t k;
+#if BZR_TRACE_WIDE
+      npend = bundle_batch<kCap, 16>(near_tier ? m.wide_near : m.wide, L.stack, sp, L.pend, L.bundle, lane, full, k);
+#else
       npend = bundle_batch<kCap>(kids, L.stack, sp, L.pend, L.bundle, lane, full, k);
+#endif
       if (full) ovf |= act;  // traversal stack exhausted: every active lane takes the full scan
       if (kCount) ctr.nodes += k;
     }
@@ -2297,7 +2326,7 @@ struct DeviceGuard {
 
 MeshView view_of(const bzr_mesh *m, float ri = 1.0f) {
   return MeshView{m->planar, m->full, m->nodes, m->leaf, m->nodes_near, m->leaf_near, m->obb, m->obb_near,
-                  m->always, m->kids, m->kids_near, m->n_always, m->n, m->s_max, m->s_near, ri};
+                  m->always, m->kids, m->kids_near, m->wide, m->wide_near, m->n_always, m->n, m->s_max, m->s_near, ri};
 }
 unsigned grid_for(uint32_t n) { return (n + kBlock - 1) / kBlock; }
 size_t round256(size_t b) { return (b + 255) & ~size_t(255); }
@@ -2778,6 +2807,43 @@ extern "C" bzr_status bzr_mesh_create(bzr_ctx *ctx, const void *patches, uint32_
     return k;
   };
   const std::vector<float4> kids = kids_of(bvh), kids_near = kids_of(bvh_near);
+  // two levels per node (k_traverse's bundle walk, BZR_TRAV_WIDE): slot 4 c + g of node i is grandchild g of
+  // its child c when that child is an axis-aligned inner node, else (a leaf, an oriented-box node) slot 4 c
+  // is the child itself and 4 c + 1..3 are empty.  A walk over these slots skips the children's own boxes,
+  // so it reaches a superset of the leaves the 4-wide walk reaches (every leaf still takes its exact gate).
+  auto wide_of = [](bzr_host::Bvh const &t) {
+    std::vector<float4> k(t.nodes4.size() * 32);
+    float empty;
+    const uint32_t e = bzr_host::kEmptyChild;
+    std::memcpy(&empty, &e, 4);
+    for (size_t i = 0; i < t.nodes4.size(); ++i) {
+      auto const &nd = t.nodes4[i];
+      for (int c = 0; c < 4; ++c) {
+        const uint32_t ch = nd.child[c];
+        const bool inner = ch != bzr_host::kEmptyChild && !(ch & (bzr_host::kLeafFlag | bzr_host::kObbFlag));
+        for (int g = 0; g < 4; ++g) {
+          float4 lo = make_float4(0.0f, 0.0f, 0.0f, empty), hi = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+          if (inner) {
+            auto const &sub = t.nodes4[ch];
+            float ref;
+            std::memcpy(&ref, &sub.child[g], 4);
+            lo = make_float4(sub.lo[0][g], sub.lo[1][g], sub.lo[2][g], ref);
+            hi = make_float4(sub.hi[0][g], sub.hi[1][g], sub.hi[2][g], 0.0f);
+          } else if (g == 0) {
+            float ref;
+            std::memcpy(&ref, &nd.child[c], 4);
+            lo = make_float4(nd.lo[0][c], nd.lo[1][c], nd.lo[2][c], ref);
+            hi = make_float4(nd.hi[0][c], nd.hi[1][c], nd.hi[2][c], 0.0f);
+          }
+          k[32 * i + 2 * (4 * c + g)] = lo;
+          k[32 * i + 2 * (4 * c + g) + 1] = hi;
+        }
+      }
+    }
+    return k;
+  };
+  const std::vector<float4> wide = BZR_TRAV_WIDE ? wide_of(bvh) : std::vector<float4>(),
+                            wide_near = BZR_TRAV_WIDE ? wide_of(bvh_near) : std::vector<float4>();
   // the always list: the same patches in both tiers (whether a gate region is proven does not depend on
   // the tier's origin radius)
   if (bvh.always != bvh_near.always) return set_error(BZR_ERR_INVALID_ARGUMENT, "BVH tiers disagree on the always list");
@@ -2815,6 +2881,8 @@ extern "C" bzr_status bzr_mesh_create(bzr_ctx *ctx, const void *patches, uint32_
       {reinterpret_cast<void **>(&mesh->always), always.data(), always.size() * sizeof(float4)},
       {reinterpret_cast<void **>(&mesh->kids), kids.data(), kids.size() * sizeof(float4)},
       {reinterpret_cast<void **>(&mesh->kids_near), kids_near.data(), kids_near.size() * sizeof(float4)},
+      {reinterpret_cast<void **>(&mesh->wide), wide.data(), wide.size() * sizeof(float4)},
+      {reinterpret_cast<void **>(&mesh->wide_near), wide_near.data(), wide_near.size() * sizeof(float4)},
   };
   hipError_t e = hipSuccess;
   for (auto &u : ups) {
@@ -2846,6 +2914,8 @@ extern "C" bzr_status bzr_mesh_destroy(bzr_mesh *mesh) {
   (void)hipFree(mesh->always);
   (void)hipFree(mesh->kids);
   (void)hipFree(mesh->kids_near);
+  (void)hipFree(mesh->wide);
+  (void)hipFree(mesh->wide_near);
   delete mesh;
   return BZR_OK;
 }
