@@ -23,6 +23,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <functional>
 
 #include <cstdio>
 #include <cstring>
@@ -165,10 +166,14 @@ constexpr int kTravBlock = BZR_TRAV_BLOCK;
 #define BZR_TRAV_LEAF_PAIRS 1
 #endif
 // BZR_TRAV_WIDE (default 1): k_traverse's bundle walk takes two tree levels per batch over 16-slot records
-// (bzr_mesh wide / wide_near: each node's grandchildren), 4 nodes per batch instead of 16 nodes' children.
+// (bzr_mesh wide / wide_near: each node's grandchildren), 4 nodes per batch instead of 16 nodes' children;
+// 2: three levels over 64-slot records (one node per batch, a 4x deeper LDS stack); 0: one level.
 #ifndef BZR_TRAV_WIDE
 #define BZR_TRAV_WIDE 1
 #endif
+constexpr uint32_t kWideSlots = BZR_TRAV_WIDE == 2 ? 64u : 16u;  // slots per node of the wide records
+// k_traverse's stack: a three-level batch (BZR_TRAV_WIDE 2) can push 64 entries at once
+constexpr int kTravStack = BZR_TRAV_WIDE == 2 ? 4 * kStack : kStack;
 // BZR_TRACE_WIDE (with BZR_TRACE_BUNDLE): k_trace's bundle walk over the same two-level records.
 #ifndef BZR_TRACE_WIDE
 #define BZR_TRACE_WIDE 0
@@ -804,7 +809,7 @@ __device__ __forceinline__ uint32_t bundle_batch(const float4 *kids, uint32_t *s
   // (the lane index laundered: lane-derived addresses hoisted out of the walk stayed live across the Newton
   // passes of k_trace and cost it a wave of occupancy)
   asm volatile("" : "+v"(lane));
-  constexpr uint32_t kShift = kSlots == 16u ? 4u : 2u;
+  constexpr uint32_t kShift = kSlots == 64u ? 6u : (kSlots == 16u ? 4u : 2u);
   constexpr int kNodes = 64 / (int)kSlots;
   const uint32_t q = lane >> kShift, c = lane & (kSlots - 1u);
   // at most (kCap - sp) / (kSlots - 1) nodes (at least one), so their <= kSlots children each fit: the stack
@@ -1114,7 +1119,7 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
         if (ch[c] & bzr_host::kLeafFlag) {
           if ((threadIdx.x & 63u) == 0u) qbuf[qn] = ch[c] & ~bzr_host::kLeafFlag;
           ++qn;
-        } else if (sp < kStack) {
+        } else if (sp < kTravStack) {
           if ((threadIdx.x & 63u) == 0u) stk[sp] = ch[c];
           ++sp;
         } else if ((hm >> (threadIdx.x & 63u)) & 1ull) {
@@ -1126,9 +1131,9 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
     bool full;
     uint32_t k;
 #if BZR_TRAV_WIDE
-    qn += bundle_batch<kStack, 16>(wide, stk, sp, qbuf, bl, threadIdx.x & 63u, full, k, qn);
+    qn += bundle_batch<kTravStack, kWideSlots>(wide, stk, sp, qbuf, bl, threadIdx.x & 63u, full, k, qn);
 #else
-    qn += bundle_batch<kStack>(kids, stk, sp, qbuf, bl, threadIdx.x & 63u, full, k, qn);
+    qn += bundle_batch<kTravStack>(kids, stk, sp, qbuf, bl, threadIdx.x & 63u, full, k, qn);
 #endif
     if (full && active) cnt |= kOverflow;  // stack exhausted: every active lane takes the full scan
     if (counters) c_nodes += k;
@@ -1159,7 +1164,7 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
         list_candidate(hit[c] & planar_gate(q0, q1, q2, q3, s, d), r[15], w, n, i, cnt);
       } else {
         if (next != 0xFFFFFFFFu) {
-          if (sp < kStack) stk[sp++] = next;
+          if (sp < kTravStack) stk[sp++] = next;
           else if ((next_hm >> (threadIdx.x & 63u)) & 1ull) cnt |= kOverflow;  // stack exhausted: full scan
         }
         next = ch[c];
@@ -1285,7 +1290,7 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
 __global__ __launch_bounds__(kTravBlock) BZR_TRAV_ATTR void k_traverse(MeshView m, const float *__restrict__ rays, uint32_t ld,
                                                          uint32_t off, const uint32_t *__restrict__ alive, uint32_t n,
                                                          Work w, unsigned long long *counters) {
-  __shared__ uint32_t stack[kTravBlock / 64][kStack];
+  __shared__ uint32_t stack[kTravBlock / 64][kTravStack];
   __shared__ float bundle[kTravBlock / 64][kBundleWords];  // the wave's ray bundle (bundle walk, always list)
 #if BZR_TRAV_BUNDLE
   __shared__ uint32_t pend[kTravBlock / 64][BZR_TRAV_PRETEST ? 128 : 64];  // the bundle walk's queued leaf slots
@@ -2807,39 +2812,34 @@ extern "C" bzr_status bzr_mesh_create(bzr_ctx *ctx, const void *patches, uint32_
     return k;
   };
   const std::vector<float4> kids = kids_of(bvh), kids_near = kids_of(bvh_near);
-  // two levels per node (k_traverse's bundle walk, BZR_TRAV_WIDE): slot 4 c + g of node i is grandchild g of
-  // its child c when that child is an axis-aligned inner node, else (a leaf, an oriented-box node) slot 4 c
-  // is the child itself and 4 c + 1..3 are empty.  A walk over these slots skips the children's own boxes,
+  // two levels per node (k_traverse's bundle walk, BZR_TRAV_WIDE; three with 2): slot 4 c + g of node i is
+  // grandchild g of its child c when that child is an axis-aligned inner node, else (a leaf, an oriented-box
+  // node) slot 4 c is the child itself and 4 c + 1..3 are empty.  A walk over these slots skips the children's own boxes,
   // so it reaches a superset of the leaves the 4-wide walk reaches (every leaf still takes its exact gate).
   auto wide_of = [](bzr_host::Bvh const &t) {
-    std::vector<float4> k(t.nodes4.size() * 32);
+    constexpr uint32_t S = kWideSlots;
     float empty;
     const uint32_t e = bzr_host::kEmptyChild;
     std::memcpy(&empty, &e, 4);
-    for (size_t i = 0; i < t.nodes4.size(); ++i) {
-      auto const &nd = t.nodes4[i];
-      for (int c = 0; c < 4; ++c) {
-        const uint32_t ch = nd.child[c];
-        const bool inner = ch != bzr_host::kEmptyChild && !(ch & (bzr_host::kLeafFlag | bzr_host::kObbFlag));
-        for (int g = 0; g < 4; ++g) {
-          float4 lo = make_float4(0.0f, 0.0f, 0.0f, empty), hi = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-          if (inner) {
-            auto const &sub = t.nodes4[ch];
-            float ref;
-            std::memcpy(&ref, &sub.child[g], 4);
-            lo = make_float4(sub.lo[0][g], sub.lo[1][g], sub.lo[2][g], ref);
-            hi = make_float4(sub.hi[0][g], sub.hi[1][g], sub.hi[2][g], 0.0f);
-          } else if (g == 0) {
+    std::vector<float4> k(t.nodes4.size() * 2 * S, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+    for (size_t s = 0; s < k.size(); s += 2) k[s].w = empty;
+    // slots [base, base + span) of node i's record: child c of nd, expanded while span > 1 and it is an
+    // axis-aligned inner node, else in the range's first slot
+    std::function<void(size_t, uint32_t, uint32_t, const bzr_host::Bvh4Node &, int)> fill =
+        [&](size_t i, uint32_t base, uint32_t span, const bzr_host::Bvh4Node &nd, int c) {
+          const uint32_t ch = nd.child[c];
+          const bool inner = ch != bzr_host::kEmptyChild && !(ch & (bzr_host::kLeafFlag | bzr_host::kObbFlag));
+          if (!inner || span == 1u) {
             float ref;
             std::memcpy(&ref, &nd.child[c], 4);
-            lo = make_float4(nd.lo[0][c], nd.lo[1][c], nd.lo[2][c], ref);
-            hi = make_float4(nd.hi[0][c], nd.hi[1][c], nd.hi[2][c], 0.0f);
+            k[2 * (S * i + base)] = make_float4(nd.lo[0][c], nd.lo[1][c], nd.lo[2][c], ref);
+            k[2 * (S * i + base) + 1] = make_float4(nd.hi[0][c], nd.hi[1][c], nd.hi[2][c], 0.0f);
+            return;
           }
-          k[32 * i + 2 * (4 * c + g)] = lo;
-          k[32 * i + 2 * (4 * c + g) + 1] = hi;
-        }
-      }
-    }
+          for (int g = 0; g < 4; ++g) fill(i, base + g * (span / 4u), span / 4u, t.nodes4[ch], g);
+        };
+    for (size_t i = 0; i < t.nodes4.size(); ++i)
+      for (int c = 0; c < 4; ++c) fill(i, c * (S / 4u), S / 4u, t.nodes4[i], c);
     return k;
   };
   const std::vector<float4> wide = BZR_TRAV_WIDE ? wide_of(bvh) : std::vector<float4>(),
