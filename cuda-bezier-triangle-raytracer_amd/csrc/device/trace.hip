@@ -1325,8 +1325,9 @@ struct BucketSplit {
 // 64 dense_base(b) + r while r < 64 dense_chunks(b), else sparse pair r - 64 dense_chunks(b) of the bucket.
 __global__ __launch_bounds__(kBlock) void k_place(uint32_t n, uint32_t nb, Work w, uint32_t *__restrict__ pair_count) {
   const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+  uint32_t c = 0;
   if (t < nb) {
-    const uint32_t c = w.hist[t];
+    c = w.hist[t];
     if (c) {
       w.hist[t] = 0u;
       if ((c & 63u) >= kDenseMin) {
@@ -1335,25 +1336,28 @@ __global__ __launch_bounds__(kBlock) void k_place(uint32_t n, uint32_t nb, Work 
       }
     }
   }
-  const uint32_t cw = t < n ? w.count[t] : 0u;
-  const uint32_t cnt = cw > kMaxCand ? 0u : cw;  // (an overflow ray's list is not ranked: the full scan takes it)
-  if (pair_count) {  // the wave's listed pairs (bzr_ctx_counters "pairs": the pairs the Newton stage runs)
-    uint32_t sum = cnt;
+  // the wave's buckets' pairs (bzr_ctx_counters "pairs": the pairs the Newton stage runs): one atomic per
+  // bucket wave -- per ray wave, the atomics on one address cost k_place 30 %
+  if (pair_count && blockIdx.x * kBlock < nb) {
+    uint32_t sum = c;
 #pragma unroll
     for (int k = 32; k >= 1; k >>= 1) sum += __shfl_xor(sum, k, 64);
     if ((threadIdx.x & 63u) == 0u && sum) atomicAdd(pair_count, sum);
   }
+  if (t >= n) return;
+  const uint32_t cnt = w.count[t];
+  if (cnt > kMaxCand || cnt == 0) return;  // (an overflow ray's list is not ranked: the full scan takes it)
   const unsigned long long tot = w.offs[nb];
   const uint32_t sparse0 = static_cast<uint32_t>(tot >> 32) * 64u;  // the sparse region's first pair
   // four list slots per round: their loads first, then the offsets, then the stores
-  for (uint32_t j0 = 0; __any(j0 < cnt); j0 += 4u) {
+  for (uint32_t j0 = 0; j0 < cnt; j0 += 4u) {
     uint32_t b[4], r[4];
     unsigned long long o0[4], o1[4];
 #pragma unroll
     for (uint32_t k = 0; k < 4u; ++k) {
-      const uint32_t j = j0 + k < cnt ? j0 + k : 0u;
-      b[k] = cnt ? w.cand[(size_t)j * n + t] : 0u;
-      r[k] = cnt ? w.rank[(size_t)j * n + t] : 0u;
+      const uint32_t j = j0 + k < cnt ? j0 + k : j0;
+      b[k] = w.cand[(size_t)j * n + t];
+      r[k] = w.rank[(size_t)j * n + t];
     }
 #pragma unroll
     for (uint32_t k = 0; k < 4u; ++k) {
