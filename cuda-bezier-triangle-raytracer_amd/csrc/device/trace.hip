@@ -1487,7 +1487,27 @@ __global__ __launch_bounds__(kBlock) void k_newton_lane(const float *__restrict_
 }
 
 template <int kMode, bool kFast>
-__global__ __launch_bounds__(kBlock) void k_finish(MeshView m, const float *rays, uint32_t ld, uint32_t off, uint32_t n,
+// BZR_FINISH_WPE / BZR_RESOLVE_WPE (A/B knobs, default 0 = the compiler's choice): amdgpu_waves_per_eu lower
+// bounds for k_finish (112 VGPRs -- the overflow rays' Newton re-evaluation -- so 4 waves per SIMD) and
+// k_resolve (120 VGPRs, 4 waves).  k_finish at 6 or 8 waves (27 / 72 VGPRs spilled) measured no faster -- it
+// is HBM-bound at ~6 TB/s either way (profiles/r04_ab_finish_split.jsonl); k_resolve spills 143 / 378.
+#ifndef BZR_FINISH_WPE
+#define BZR_FINISH_WPE 0
+#endif
+#ifndef BZR_RESOLVE_WPE
+#define BZR_RESOLVE_WPE 0
+#endif
+#if BZR_FINISH_WPE
+#define BZR_FINISH_ATTR __attribute__((amdgpu_waves_per_eu(BZR_FINISH_WPE)))
+#else
+#define BZR_FINISH_ATTR
+#endif
+#if BZR_RESOLVE_WPE
+#define BZR_RESOLVE_ATTR __attribute__((amdgpu_waves_per_eu(BZR_RESOLVE_WPE)))
+#else
+#define BZR_RESOLVE_ATTR
+#endif
+__global__ __launch_bounds__(kBlock) BZR_FINISH_ATTR void k_finish(MeshView m, const float *rays, uint32_t ld, uint32_t off, uint32_t n,
                                                    Work w, Out o) {
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   if (blockIdx.x == 0 && threadIdx.x < 4) w.ctr[threadIdx.x] = 0u;  // last reader of the counters this segment
@@ -1543,7 +1563,7 @@ __device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v)
 // blocks take (overflow ray, patch slice) items.  With no overflow rays the second loop is empty --
 // one launch per segment saved over separate kernels.
 template <bool kFast>
-__global__ __launch_bounds__(kBlock) void k_resolve(MeshView m, const float *__restrict__ rays, uint32_t ld,
+__global__ __launch_bounds__(kBlock) BZR_RESOLVE_ATTR void k_resolve(MeshView m, const float *__restrict__ rays, uint32_t ld,
                                                     uint32_t off, uint32_t n, Work w) {
   const uint32_t F = __builtin_amdgcn_readfirstlane(w.ctr[0]);
   for (uint32_t q = blockIdx.x * kBlock + threadIdx.x; q < F; q += gridDim.x * kBlock) {
