@@ -174,9 +174,9 @@ constexpr int kTravBlock = BZR_TRAV_BLOCK;
 constexpr uint32_t kWideSlots = BZR_TRAV_WIDE == 2 ? 64u : 16u;  // slots per node of the wide records
 // k_traverse's stack: a three-level batch (BZR_TRAV_WIDE 2) can push 64 entries at once
 constexpr int kTravStack = BZR_TRAV_WIDE == 2 ? 4 * kStack : kStack;
-// BZR_TRACE_WIDE (with BZR_TRACE_BUNDLE): k_trace's bundle walk over the same two-level records.
+// BZR_TRACE_WIDE (default 1, with BZR_TRACE_BUNDLE): k_trace's bundle walk over the same two-level records.
 #ifndef BZR_TRACE_WIDE
-#define BZR_TRACE_WIDE 0
+#define BZR_TRACE_WIDE 1
 #endif
 // BZR_TRAV_BUNDLE (default 1): k_traverse walks with the wave-bundle test in batches (traverse_rays):
 // cfg5 8192^2 staged k_traverse 6.61 -> 5.07 ms per frame, cfg3 0.283 -> 0.235, cfg2 0.134 -> 0.143
@@ -1687,14 +1687,16 @@ struct TraceCtr {  // wave-uniform work counters (kCount)
 #endif
 // BZR_TRACE_PARK_HITS (default 1): park cNone results in the intersect kernel (kModeHits) as well: cfg5
 // fused -7.8 % Newton passes, +3.2 % Mrays/s; cfg3 +1 % (profiles/r03_ab_cfg{5,3}_fused_parkhits.jsonl).
-// BZR_TRACE_BUNDLE (default 0): k_trace walks the tree with the wave-bundle test in batches of up to 16
-// nodes (trace_segment) instead of one node at a time with each lane's slab test.  Measured (same bits,
-// profiles/r03s2_ab_trace_bundle.jsonl): cfg5 fused -7 % (29 node visits per wave-segment become ~10
-// batches), but cfg4 +5 to +6 %, cfg2 +2.6 to +3.4 %, cfg3 +1.7 % -- a coherent wave in a 6144-patch lens
-// visits only ~13 nodes, and the bundle setup (12 DPP reductions) and batch bookkeeping cost what the
-// fewer slab tests save -- at 7 waves per SIMD (waves_per_eu(7): 72 VGPRs) as at 6.  Off.
+// BZR_TRACE_BUNDLE (default 1): k_trace walks the tree with the wave-bundle test in batches (trace_segment)
+// instead of one node at a time with each lane's slab test (0; rim waves whose bundle is wide take that walk
+// anyway).  Round 3 measured the 4-wide bundle walk slower on the chains (cfg4 +5 to +6 %, cfg2 +3 %; cfg5
+// fused -7 %, profiles/r03s2_ab_trace_bundle.jsonl): the bundle setup and the per-level batches cost what
+// the fewer slab tests saved.  Round 4's integer DPP reductions and two-level batches (BZR_TRACE_WIDE) turn
+// it around: bench.py with frames in flight, same bits, cfg4 11 074 -> 11 525 Mrays/s (+4.1 %), cfg2 +1.1 %,
+// cfg5 fused +14 %, cfg3 fused +0.7 % (profiles/r04_bench_ab_trace_wide.jsonl; one serialized frame is
+// within 1 %: the walk's VALU is what overlapping frames compete for).
 #ifndef BZR_TRACE_BUNDLE
-#define BZR_TRACE_BUNDLE 0
+#define BZR_TRACE_BUNDLE 1
 #endif
 #ifndef BZR_TRACE_PARK_HITS
 #define BZR_TRACE_PARK_HITS 1

@@ -15,9 +15,10 @@ rpl2 / rpl4: libbzr whose fused kernel is k_trace_r (trace_pool.inc): 2 or 4 ray
 pooled over a wave's 128 / 256 rays (-DBZR_TRACE_RPL); the same checks plus cfg4's two-lens chain and origins
 beyond s_max (the in-order scan inside the pooled kernel), fused == brute force == the oracle.
 
-tracebundle: libbzr with k_trace's wave-bundle walk (-DBZR_TRACE_BUNDLE=1, off by default; k_traverse uses
-it by default): the same checks, fused == staged == brute force (== the oracle on cfg2), including the
-incoherent cfg5 rays whose wide bundles take the per-lane node tests.
+tracebundle / traceperlane: libbzr with k_trace's wave-bundle walk one tree level per batch (-DBZR_TRACE_WIDE=0;
+the default takes two) and with k_trace's per-lane walk (-DBZR_TRACE_BUNDLE=0, round 3's default): the same
+checks, fused == staged == brute force (== the oracle on cfg2), including the incoherent cfg5 rays whose wide
+bundles take the per-lane node tests.
 
 The variant runs in a child process (BZR_LIBRARY selects the library; one process = one libbzr).
 """
@@ -129,11 +130,13 @@ def test_tiny_stack_overflow_path_is_exact():
 
 
 @pytest.mark.gpu
-def test_trace_bundle_walk_is_exact():
-    """The wave-bundle walk in k_trace: exact, and only the far origins take the in-order scan (round 3's
-    4096-of-1026 count came from a pre-release bundle walk whose full-stack batches sent whole incoherent
-    waves to the scan; the released one tests wide bundles per lane -- profiles/r04_bundle_overflow_probe.jsonl)."""
-    lib = PKG / "lib" / "tracebundle" / "libbzr.so"
+@pytest.mark.parametrize("variant", ["tracebundle", "traceperlane"])
+def test_trace_bundle_walk_is_exact(variant):
+    """k_trace's other walks (one level per batch; per lane): exact, and only the far origins take the in-order
+    scan (round 3's 4096-of-1026 count came from a pre-release bundle walk whose full-stack batches sent whole
+    incoherent waves to the scan; the released one tests wide bundles per lane --
+    profiles/r04_bundle_overflow_probe.jsonl)."""
+    lib = PKG / "lib" / variant / "libbzr.so"
     if not lib.exists():
         pytest.fail(f"{lib} missing: build() makes the `variants` target")
     env = dict(os.environ, BZR_LIBRARY=str(lib))
