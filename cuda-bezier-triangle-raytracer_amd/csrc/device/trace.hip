@@ -174,6 +174,10 @@ constexpr int kTravBlock = BZR_TRAV_BLOCK;
 constexpr uint32_t kWideSlots = BZR_TRAV_WIDE == 2 ? 64u : 16u;  // slots per node of the wide records
 // k_traverse's stack: a three-level batch (BZR_TRAV_WIDE 2) can push 64 entries at once
 constexpr int kTravStack = BZR_TRAV_WIDE == 2 ? 4 * kStack : kStack;
+// BZR_TRACE_BLEAF_PAIRS (A/B knob, default 0): k_trace's bundle walk gate-tests its queued leaves two at a time.
+#ifndef BZR_TRACE_BLEAF_PAIRS
+#define BZR_TRACE_BLEAF_PAIRS 0
+#endif
 // BZR_TRACE_WIDE (default 1, with BZR_TRACE_BUNDLE): k_trace's bundle walk over the same two-level records.
 #ifndef BZR_TRACE_WIDE
 #define BZR_TRACE_WIDE 1
@@ -1887,6 +1891,41 @@ __device__ __forceinline__ void trace_segment(const MeshView &m, f3 s, f3 d, boo
 #if BZR_TRACE_BUNDLE
     while (bwalk && ne < kEntries) {
       if (pi < npend) {  // a queued leaf: every active lane's planar gate
+#if BZR_TRACE_BLEAF_PAIRS
+        // two queued leaves per step when the entry list has room for both: both records in flight, one wait
+        const bool two = pi + 1u < npend && ne + 1u < kEntries;
+        const uint32_t slot0 = __builtin_amdgcn_readfirstlane(L.pend[pi]);
+        const uint32_t slot1 = __builtin_amdgcn_readfirstlane(L.pend[two ? pi + 1u : pi]);
+        pi += two ? 2u : 1u;
+        u32x16 r0, r1;
+        asm volatile("s_load_dwordx16 %0, %2, 0x0\n\ts_load_dwordx16 %1, %3, 0x0\n\ts_waitcnt lgkmcnt(0)"
+                     : "=&s"(r0), "=&s"(r1)
+                     : "s"(leaf + 4u * slot0), "s"(leaf + 4u * slot1));
+        if (kCount) {
+          ctr.leaves += two ? 2u : 1u;
+          ctr.gate_tests += (two ? 2u : 1u) * popc64(__ballot(act));
+        }
+        const unsigned long long pm0 =
+            __ballot(act & planar_gate(leaf_q(r0, 0), leaf_q(r0, 1), leaf_q(r0, 2), leaf_q(r0, 3), s, d));
+        if (pm0) {
+          if (lane == 0u) {
+            L.eid[ne] = r0[15];
+            L.emask[ne] = pm0;
+          }
+          ++ne;
+        }
+        if (two) {
+          const unsigned long long pm1 =
+              __ballot(act & planar_gate(leaf_q(r1, 0), leaf_q(r1, 1), leaf_q(r1, 2), leaf_q(r1, 3), s, d));
+          if (pm1) {
+            if (lane == 0u) {
+              L.eid[ne] = r1[15];
+              L.emask[ne] = pm1;
+            }
+            ++ne;
+          }
+        }
+#else
         const uint32_t slot = __builtin_amdgcn_readfirstlane(L.pend[pi]);
         ++pi;
         const u32x16 r = *((const cu32x16 *)(uintptr_t)leaf + slot);
@@ -1903,6 +1942,7 @@ __device__ __forceinline__ void trace_segment(const MeshView &m, f3 s, f3 d, boo
           }
           ++ne;
         }
+#endif
         continue;
       }
       if (sp == 0) break;
