@@ -175,6 +175,8 @@ constexpr uint32_t kWideSlots = BZR_TRAV_WIDE == 2 ? 64u : 16u;  // slots per no
 // k_traverse's stack: a three-level batch (BZR_TRAV_WIDE 2) can push 64 entries at once
 constexpr int kTravStack = BZR_TRAV_WIDE == 2 ? 4 * kStack : kStack;
 // BZR_TRACE_BLEAF_PAIRS (A/B knob, default 0): k_trace's bundle walk gate-tests its queued leaves two at a time.
+// Measured at bench level: cfg4 -4.1 %, cfg2 -2.7 %, cfg5 fused -3.4 % (80 VGPRs with 5 spilled to scratch,
+// 49 SGPR spills; profiles/r04_bench_ab_trace_leaf_pairs.jsonl) -- unlike k_traverse, where pairs pay.
 #ifndef BZR_TRACE_BLEAF_PAIRS
 #define BZR_TRACE_BLEAF_PAIRS 0
 #endif
