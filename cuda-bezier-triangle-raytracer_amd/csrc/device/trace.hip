@@ -132,9 +132,12 @@ __device__ __forceinline__ uint32_t deal_blocks(uint32_t b, uint32_t nblocks) {
     return (k / kPolicy * kXcds + x) * kPolicy + k % kPolicy;
   }
 }
-// Threads per k_traverse block: its waves share one CU (scalar cache) and take neighbouring rays.
+// Threads per k_traverse block (BZR_TRAV_BLOCK, default 64): one-wave blocks let a finished wave be replaced
+// at once, as in k_trace; 256 (4 waves sharing a CU's scalar cache on neighbouring rays, rounds 1-3) measured
+// 0.5-1 % slower on cfg5 and 0.1-0.2 % on cfg3 at bench level, 128 4 % slower on cfg3
+// (profiles/r04_bench_ab_trav_block.jsonl).
 #ifndef BZR_TRAV_BLOCK
-#define BZR_TRAV_BLOCK 256
+#define BZR_TRAV_BLOCK 64
 #endif
 constexpr int kTravBlock = BZR_TRAV_BLOCK;
 // BZR_SLAB_FMA (default 1): the traversal slab test as fma(lo, inv, -s*inv) (mirrored by bvh.cpp slab_h).
