@@ -98,7 +98,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=10)
-    p.add_argument("--prewarm-s", type=float, default=0.3,
+    p.add_argument("--prewarm-s", type=float, default=4.0,
                    help="seconds of back-to-back frames before the warmup steps (clock ramp), 0 = off")
     p.add_argument("--config", default="cfg4", choices=["cfg2", "cfg3", "cfg4", "cfg5"])
     p.add_argument("--side", type=int, default=0, help="override rays per image side")

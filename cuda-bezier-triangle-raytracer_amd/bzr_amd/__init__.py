@@ -433,12 +433,12 @@ def trace_tiled(ctxs, lenses, ri, rays, tile_rays=4096, mode=MODE_PARITY, out=No
     return out
 
 
-GATHER_AUTO, GATHER_RCCL, GATHER_PEER = 0, 1, 2  # BZR_GATHER_*
+GATHER_AUTO, GATHER_RCCL, GATHER_PEER, GATHER_DIRECT = 0, 1, 2, 3  # BZR_GATHER_*
 
 
 class TiledPlan:
     """bzr_tiled: multi-device frames from one process, gathered to device 0 on the device side (RCCL over
-    xGMI between distinct devices, peer copies otherwise).  ctxs: nslot lists of ndev contexts (slot s, device
+    xGMI between distinct devices, peer copies otherwise; one device: traced straight into the outputs).  ctxs: nslot lists of ndev contexts (slot s, device
     d); the frame is n tile-major rays."""
 
     def __init__(self, ctxs, n: int, tile_rays: int = 4096, transport: int = GATHER_AUTO):

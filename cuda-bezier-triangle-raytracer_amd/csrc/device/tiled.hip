@@ -18,6 +18,9 @@
 // same slot packs only after that slot's previous gather has left the buffer, device 0's stream of the
 // gather serialises the receive buffers.  Bytes: 28 per primary cross to device 0, (ndev - 1) / ndev of them
 // over xGMI.  Byte work only: the kernels here are HBM-bound copies.
+// A one-device plan (BZR_GATHER_DIRECT, AUTO's choice for ndev == 1) skips steps 2-4: its share is the frame
+// in frame order, so each frame is one bzr_trace_chain from the resident rays into the caller's outputs.
+// bzr_tiled_set_rays lands the frame on device 0 once and sends every other device only its share.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -231,12 +234,15 @@ struct bzr_tiled {
   std::vector<uint32_t> share;       // rays of device d's share
   std::vector<float *> in;           // [d] share input rays [6][share]
   struct Slot {
-    std::vector<float *> rays;       // [d] chain outputs
+    std::vector<float *> rays;       // [d] chain outputs (not allocated by a DIRECT plan)
     std::vector<uint32_t *> status, segments;
     std::vector<float *> packed;     // [d] [7][npad]
     float *recv = nullptr;           // device 0: [ndev][7][npad]
-    std::vector<hipEvent_t> packed_ev;  // [d] on ctx stream: share packed
-    std::vector<hipEvent_t> sent_ev;    // [d] on the gather stream of d: packed buffer free again
+    std::vector<hipEvent_t> packed_ev;  // [d] on ctx stream: share packed (DIRECT: [0] the frame traced)
+    // [d] the packed buffer is free again; created on the device of the stream that records it (RCCL: the
+    // gather stream of d, on dev[d]; peer: gstream[0], on dev[0]) -- HIP records an event only on a stream of
+    // the event's own device
+    std::vector<hipEvent_t> sent_ev;
     bool used = false;
   };
   std::vector<Slot> slot;
@@ -249,7 +255,13 @@ struct bzr_tiled {
   int32_t layout = BZR_PACK_RAYS;
   uint32_t cap = 0, cpad = 0;        // compact: capacity; npad rounded up to a multiple of 4 (byte words)
   size_t words = 0;                  // floats of one packed share (the allocation: the larger layout)
-  float *prim0 = nullptr;            // device 0: the frame's primary rays [6][n] (bzr_tiled_set_rays)
+  // device 0: the frame's primary rays [6][n] (bzr_tiled_set_rays) -- prim_buf with several devices; with
+  // one device the share is the frame in frame order, so prim0 is in[0] itself
+  float *prim0 = nullptr, *prim_buf = nullptr;
+  float *stage = nullptr;            // device 0: the other devices' shares before their peer copies
+  hipEvent_t rays_ev = nullptr;      // device 0, on ctxs[0]'s stream: the last set_rays' copies are queued before it
+  uint64_t rays_gen = 0;             // set_rays calls so far; rays_seen[k]: the last one context k's stream waited for
+  std::vector<uint64_t> rays_seen;
   bool prim_valid = false;
   uint32_t *dshare = nullptr;        // device 0: share sizes [ndev]
   uint32_t *unpack = nullptr;        // device 0: compact block counts / offsets [2][ndev][nblk], overflow flag
@@ -286,13 +298,15 @@ struct bzr_tiled {
     }
     if (!dev.empty()) {
       free_on(dev[0], host_out);
-      free_on(dev[0], prim0);
+      free_on(dev[0], prim_buf);
+      free_on(dev[0], stage);
       free_on(dev[0], dshare);
       free_on(dev[0], unpack);
     }
     for (uint32_t d = 0; d < gstream.size(); ++d)
       if (gstream[d]) (void)hipStreamDestroy(gstream[d]);
     if (done) (void)hipEventDestroy(done);
+    if (rays_ev) (void)hipEventDestroy(rays_ev);
   }
 };
 
@@ -311,6 +325,7 @@ bzr_status alloc_on(int device, T *&p, size_t count) {
 bzr_status build(bzr_tiled &t, bzr_ctx *const *ctxs, int32_t transport) {
   const uint32_t ndev = t.ndev;
   t.ctxs.assign(ctxs, ctxs + (size_t)ndev * t.nslot);
+  t.rays_seen.assign(t.ctxs.size(), 0);
   for (uint32_t d = 0; d < ndev; ++d) t.dev.push_back(ctxs[d]->device);
   for (uint32_t s = 1; s < t.nslot; ++s)
     for (uint32_t d = 0; d < ndev; ++d)
@@ -319,10 +334,14 @@ bzr_status build(bzr_tiled &t, bzr_ctx *const *ctxs, int32_t transport) {
   bool distinct = true;
   for (uint32_t d = 0; d < ndev; ++d)
     if (std::count(t.dev.begin(), t.dev.end(), t.dev[d]) > 1) distinct = false;
-  if (transport == BZR_GATHER_AUTO) transport = distinct ? BZR_GATHER_RCCL : BZR_GATHER_PEER;
+  if (transport == BZR_GATHER_AUTO)
+    transport = ndev == 1 ? BZR_GATHER_DIRECT : distinct ? BZR_GATHER_RCCL : BZR_GATHER_PEER;
   if (transport == BZR_GATHER_RCCL && !distinct)
     return fail(BZR_ERR_INVALID_ARGUMENT, "bzr_tiled_create: RCCL needs distinct devices (use BZR_GATHER_PEER)");
+  if (transport == BZR_GATHER_DIRECT && ndev != 1)
+    return fail(BZR_ERR_INVALID_ARGUMENT, "bzr_tiled_create: BZR_GATHER_DIRECT is the one-device plan");
   t.transport = transport;
+  const bool direct = transport == BZR_GATHER_DIRECT;
 
   // the deal: tile k -> device k % ndev
   const uint32_t tiles = (t.n + t.tile_rays - 1) / t.tile_rays;
@@ -336,6 +355,7 @@ bzr_status build(bzr_tiled &t, bzr_ctx *const *ctxs, int32_t transport) {
   t.in.assign(ndev, nullptr);
   for (uint32_t d = 0; d < ndev; ++d)
     if (bzr_status s = alloc_on(t.dev[d], t.in[d], (size_t)6 * t.share[d])) return s;
+  if (ndev == 1) t.prim0 = t.in[0];  // one device: its share is the frame, in frame order
   t.slot.resize(t.nslot);
   for (auto &sl : t.slot) {
     sl.rays.assign(ndev, nullptr);
@@ -345,15 +365,21 @@ bzr_status build(bzr_tiled &t, bzr_ctx *const *ctxs, int32_t transport) {
     sl.packed_ev.assign(ndev, nullptr);
     sl.sent_ev.assign(ndev, nullptr);
     for (uint32_t d = 0; d < ndev; ++d) {
-      if (bzr_status s = alloc_on(t.dev[d], sl.rays[d], (size_t)6 * t.share[d])) return s;
-      if (bzr_status s = alloc_on(t.dev[d], sl.status[d], t.share[d])) return s;
-      if (bzr_status s = alloc_on(t.dev[d], sl.segments[d], t.share[d])) return s;
-      if (bzr_status s = alloc_on(t.dev[d], sl.packed[d], t.words)) return s;
-      DeviceGuard g(t.dev[d]);
-      TILED_HIP(hipEventCreateWithFlags(&sl.packed_ev[d], hipEventDisableTiming));
+      if (!direct) {  // a DIRECT frame is traced into the caller's outputs: no share outputs, no packing
+        if (bzr_status s = alloc_on(t.dev[d], sl.rays[d], (size_t)6 * t.share[d])) return s;
+        if (bzr_status s = alloc_on(t.dev[d], sl.status[d], t.share[d])) return s;
+        if (bzr_status s = alloc_on(t.dev[d], sl.segments[d], t.share[d])) return s;
+        if (bzr_status s = alloc_on(t.dev[d], sl.packed[d], t.words)) return s;
+      }
+      {
+        DeviceGuard g(t.dev[d]);
+        TILED_HIP(hipEventCreateWithFlags(&sl.packed_ev[d], hipEventDisableTiming));
+      }
+      DeviceGuard g(t.transport == BZR_GATHER_RCCL ? t.dev[d] : t.dev[0]);  // the device of the recording stream
       TILED_HIP(hipEventCreateWithFlags(&sl.sent_ev[d], hipEventDisableTiming));
     }
-    if (bzr_status s = alloc_on(t.dev[0], sl.recv, (size_t)ndev * t.words)) return s;
+    if (!direct)
+      if (bzr_status s = alloc_on(t.dev[0], sl.recv, (size_t)ndev * t.words)) return s;
   }
   const uint32_t nstreams = t.transport == BZR_GATHER_RCCL ? ndev : 1u;
   t.gstream.assign(nstreams, nullptr);
@@ -364,6 +390,7 @@ bzr_status build(bzr_tiled &t, bzr_ctx *const *ctxs, int32_t transport) {
   {
     DeviceGuard g(t.dev[0]);
     TILED_HIP(hipEventCreateWithFlags(&t.done, hipEventDisableTiming));
+    TILED_HIP(hipEventCreateWithFlags(&t.rays_ev, hipEventDisableTiming));
     if (bzr_status s = alloc_on(t.dev[0], t.dshare, ndev)) return s;
     if (bzr_status s = alloc_on(t.dev[0], t.unpack, (size_t)2 * ndev * t.nblk + 1)) return s;
     TILED_HIP(hipMemcpy(t.dshare, t.share.data(), ndev * sizeof(uint32_t), hipMemcpyHostToDevice));
@@ -436,73 +463,47 @@ extern "C" bzr_status bzr_tiled_set_rays(bzr_tiled *t, const float *rays, uint32
   if (!t) return fail(BZR_ERR_INVALID_ARGUMENT, "bzr_tiled_set_rays: null plan");
   if (!rays) return fail(BZR_ERR_INVALID_ARGUMENT, "bzr_tiled_set_rays: null rays");
   if (flags & ~uint32_t(BZR_DEVICE_PTRS)) return fail(BZR_ERR_INVALID_ARGUMENT, "bzr_tiled_set_rays: unknown flags");
+  // frames in flight read the share inputs and device 0's frame copy: they finish first
+  if (bzr_status s = bzr_tiled_sync(t)) return s;
+  t->prim_valid = false;
   const size_t bytes = (size_t)6 * t->n * sizeof(float);
-  // the whole frame on each device (host: H2D; device 0: peer copies), then each device extracts its share
-  const float *src0 = rays;
-  float *stage0 = nullptr;
+  // Device 0 keeps the whole frame (the compact layout returns a ray that never refracted from it): one copy
+  // there, then device 0 extracts every share and sends each other device only its own -- (ndev - 1) / ndev
+  // of the frame over xGMI in all.  Everything is queued on ctxs[0]'s stream; rays_ev orders the slots'
+  // next frames after it, with no host wait (a host source is waited for, so the caller may reuse it).
+  if (t->ndev > 1 && !t->prim_buf)
+    if (bzr_status s = alloc_on(t->dev[0], t->prim_buf, (size_t)6 * t->n)) return s;
+  if (t->ndev > 1) t->prim0 = t->prim_buf;
+  size_t stage_words = 0;
+  for (uint32_t d = 1; d < t->ndev; ++d)
+    if (t->dev[d] != t->dev[0]) stage_words += (size_t)6 * t->share[d];
+  if (stage_words && !t->stage)
+    if (bzr_status s = alloc_on(t->dev[0], t->stage, stage_words)) return s;
   bzr_ctx *c0 = t->ctxs[0];
-  if (!(flags & BZR_DEVICE_PTRS)) {
-    if (bzr_status s = alloc_on(t->dev[0], stage0, (size_t)6 * t->n)) return s;
-    DeviceGuard g(t->dev[0]);
-    hipError_t e = hipMemcpyAsync(stage0, rays, bytes, hipMemcpyHostToDevice, c0->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(c0->stream);
-    if (e != hipSuccess) {
-      (void)hipFree(stage0);
-      return fail(BZR_ERR_HIP, std::string("bzr_tiled_set_rays: ") + hipGetErrorString(e));
-    }
-    src0 = stage0;
-  }
-  // device 0 keeps the whole frame: the compact layout returns a ray that never refracted from it
-  if (!t->prim0)
-    if (bzr_status s = alloc_on(t->dev[0], t->prim0, (size_t)6 * t->n)) {
-      if (stage0) {
-        DeviceGuard g(t->dev[0]);
-        (void)hipFree(stage0);
+  DeviceGuard g(t->dev[0]);
+  const bool host = !(flags & BZR_DEVICE_PTRS);
+  TILED_HIP(hipMemcpyAsync(t->prim0, rays, bytes, host ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice, c0->stream));
+  if (host) TILED_HIP(hipStreamSynchronize(c0->stream));  // the caller's host buffer has been read
+  if (t->ndev > 1) {
+    size_t off = 0;
+    for (uint32_t d = 0; d < t->ndev; ++d) {
+      if (t->share[d] == 0) continue;
+      const bool local = t->dev[d] == t->dev[0];
+      float *dst = local ? t->in[d] : t->stage + off;
+      hipLaunchKernelGGL(k_share_extract, dim3((t->share[d] + kThreads - 1) / kThreads), dim3(kThreads), 0, c0->stream,
+                         t->prim0, t->n, d, t->ndev, t->tile_rays, t->share[d], dst);
+      TILED_HIP(hipGetLastError());
+      if (!local) {
+        TILED_HIP(hipMemcpyPeerAsync(t->in[d], t->dev[d], dst, t->dev[0], (size_t)6 * t->share[d] * sizeof(float),
+                                     c0->stream));
+        off += (size_t)6 * t->share[d];
       }
-      return s;
-    }
-  {
-    DeviceGuard g(t->dev[0]);
-    hipError_t e = hipMemcpyAsync(t->prim0, src0, bytes, hipMemcpyDeviceToDevice, c0->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(c0->stream);
-    if (e != hipSuccess) {
-      if (stage0) (void)hipFree(stage0);
-      return fail(BZR_ERR_HIP, std::string("bzr_tiled_set_rays: ") + hipGetErrorString(e));
     }
   }
+  TILED_HIP(hipEventRecord(t->rays_ev, c0->stream));
+  ++t->rays_gen;
   t->prim_valid = true;
-  bzr_status result = BZR_OK;
-  for (uint32_t d = 0; d < t->ndev && result == BZR_OK; ++d) {
-    if (t->share[d] == 0) continue;
-    bzr_ctx *c = t->ctxs[d];
-    const float *src = src0;
-    float *tmp = nullptr;
-    if (t->dev[d] != t->dev[0]) {
-      if ((result = alloc_on(t->dev[d], tmp, (size_t)6 * t->n)) != BZR_OK) break;
-      DeviceGuard g(t->dev[d]);
-      hipError_t e = hipMemcpyPeerAsync(tmp, t->dev[d], src0, t->dev[0], bytes, c->stream);
-      if (e != hipSuccess) result = fail(BZR_ERR_HIP, std::string("bzr_tiled_set_rays: peer copy: ") + hipGetErrorString(e));
-      src = tmp;
-    }
-    if (result == BZR_OK) {
-      DeviceGuard g(t->dev[d]);
-      hipLaunchKernelGGL(k_share_extract, dim3((t->share[d] + kThreads - 1) / kThreads), dim3(kThreads), 0, c->stream,
-                         src, t->n, d, t->ndev, t->tile_rays, t->share[d], t->in[d]);
-      hipError_t e = hipGetLastError();
-      if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-      if (e != hipSuccess) result = fail(BZR_ERR_HIP, std::string("bzr_tiled_set_rays: ") + hipGetErrorString(e));
-    }
-    if (tmp) {
-      DeviceGuard g(t->dev[d]);
-      (void)hipFree(tmp);
-    }
-  }
-  if (stage0) {
-    DeviceGuard g(t->dev[0]);
-    (void)hipFree(stage0);
-  }
-  // every slot's stream sees the rays (the extract ran on slot 0's streams, now synchronised)
-  return result;
+  return BZR_OK;
 }
 
 namespace {
@@ -570,6 +571,43 @@ extern "C" bzr_status bzr_tiled_trace(bzr_tiled *t, const bzr_mesh *const *lense
                                           "bzr_tiled_set_rays (device 0 returns the rays that never refracted)");
   const uint32_t s = static_cast<uint32_t>(t->frames % t->nslot);
   bzr_tiled::Slot &sl = t->slot[s];
+  for (uint32_t d = 0; d < t->ndev; ++d) {  // the slot's streams see the last set_rays' copies
+    const size_t k = (size_t)s * t->ndev + d;
+    if (t->rays_seen[k] != t->rays_gen) {
+      DeviceGuard g(t->dev[d]);
+      TILED_HIP(hipStreamWaitEvent(t->ctxs[k]->stream, t->rays_ev, 0));
+      t->rays_seen[k] = t->rays_gen;
+    }
+  }
+  if (t->transport == BZR_GATHER_DIRECT) {
+    // one device: its share is the frame in frame order -- trace straight into the outputs (host outputs:
+    // device-0 staging, then copied back on the same stream), then hand the frame to the gather stream so
+    // bzr_tiled_stream keeps its meaning
+    bzr_ctx *c = t->ctxs[s];
+    float *o_rays = out_rays;
+    uint32_t *o_st = out_status, *o_seg = out_segments;
+    if (host) {
+      if (!t->host_out)
+        if (bzr_status st = alloc_on(t->dev[0], t->host_out, (size_t)8 * t->n)) return st;
+      o_rays = t->host_out;
+      o_st = reinterpret_cast<uint32_t *>(t->host_out + (size_t)6 * t->n);
+      o_seg = o_st + t->n;
+    }
+    bzr_status st = bzr_trace_chain(c, lenses, ri, nlens, t->in[0], t->n, o_rays, o_st, o_seg, flags | BZR_DEVICE_PTRS);
+    if (st != BZR_OK) return fail(st, std::string("bzr_tiled_trace: ") + bzr_last_error());
+    ++t->frames;
+    DeviceGuard g(t->dev[0]);
+    if (host) {
+      TILED_HIP(hipMemcpyAsync(out_rays, o_rays, (size_t)24 * t->n, hipMemcpyDeviceToHost, c->stream));
+      TILED_HIP(hipMemcpyAsync(out_status, o_st, (size_t)4 * t->n, hipMemcpyDeviceToHost, c->stream));
+      if (out_segments) TILED_HIP(hipMemcpyAsync(out_segments, o_seg, (size_t)4 * t->n, hipMemcpyDeviceToHost, c->stream));
+      TILED_HIP(hipStreamSynchronize(c->stream));
+      return BZR_OK;
+    }
+    TILED_HIP(hipEventRecord(sl.packed_ev[0], c->stream));
+    TILED_HIP(hipStreamWaitEvent(t->gstream[0], sl.packed_ev[0], 0));
+    return BZR_OK;
+  }
   for (uint32_t d = 0; d < t->ndev; ++d) {
     bzr_ctx *c = t->ctxs[(size_t)s * t->ndev + d];
     if (t->share[d]) {
@@ -606,6 +644,16 @@ extern "C" bzr_status bzr_tiled_trace(bzr_tiled *t, const bzr_mesh *const *lense
     TILED_HIP(hipMemcpyAsync(out_status, o_st, (size_t)4 * t->n, hipMemcpyDeviceToHost, gs));
     if (out_segments) TILED_HIP(hipMemcpyAsync(out_segments, o_seg, (size_t)4 * t->n, hipMemcpyDeviceToHost, gs));
     TILED_HIP(hipStreamSynchronize(gs));
+    if (t->layout == BZR_PACK_COMPACT) {  // a synchronous caller learns of an incomplete frame now
+      uint32_t *flag = t->unpack + (size_t)2 * t->ndev * t->nblk, h = 0;
+      TILED_HIP(hipMemcpy(&h, flag, sizeof(h), hipMemcpyDeviceToHost));
+      if (h) {
+        TILED_HIP(hipMemset(flag, 0, sizeof(h)));
+        return fail(BZR_ERR_CAPACITY, "bzr_tiled_trace: the frame had more survivors than the compact capacity " +
+                                          std::to_string(t->cap) + ": its outputs are incomplete (bzr_tiled_calibrate "
+                                          "or a larger cap)");
+      }
+    }
   }
   return BZR_OK;
 }

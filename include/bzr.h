@@ -214,14 +214,16 @@ bzr_status bzr_trace_tiled(bzr_ctx *const *ctxs, uint32_t nctx, const bzr_mesh *
 /* ---- multi-GPU frames from one process, gathered on the device (one host thread drives
  * every device, ncclCommInitAll, grouped ncclSend / ncclRecv to device 0) ---- */
 typedef struct bzr_tiled bzr_tiled;
-enum { BZR_GATHER_AUTO = 0, BZR_GATHER_RCCL = 1, BZR_GATHER_PEER = 2 };
+enum { BZR_GATHER_AUTO = 0, BZR_GATHER_RCCL = 1, BZR_GATHER_PEER = 2, BZR_GATHER_DIRECT = 3 };
 /* A frame plan over ndev devices and nslot frame slots: ctxs[s * ndev + d] is slot s's context on list
  * device d (every slot lists the same devices in the same order; all contexts distinct).  The frame is n
  * rays in tile-major order; device d traces tiles d, d + ndev, ... (its share).  The plan owns each
  * device's share buffers per slot and device 0's receive buffers.  transport: BZR_GATHER_RCCL (one RCCL
  * communicator per device, ncclCommInitAll; needs distinct devices), BZR_GATHER_PEER (hipMemcpyPeerAsync;
- * any device list, including several list entries on one device), BZR_GATHER_AUTO (RCCL when the devices
- * are distinct).  Not thread-safe; the contexts must not be used by other threads meanwhile. */
+ * any device list, including several list entries on one device), BZR_GATHER_DIRECT (ndev == 1 only: the
+ * one device traces straight into the caller's outputs -- no pack, no gather, no unpack, no share
+ * buffers), BZR_GATHER_AUTO (DIRECT for one device, RCCL when several devices are distinct, PEER
+ * otherwise).  Not thread-safe; the contexts must not be used by other threads meanwhile. */
 bzr_status bzr_tiled_create(bzr_ctx *const *ctxs, uint32_t ndev, uint32_t nslot, uint32_t n, uint32_t tile_rays,
                             int32_t transport, bzr_tiled **out);
 bzr_status bzr_tiled_destroy(bzr_tiled *plan);
@@ -229,7 +231,13 @@ bzr_status bzr_tiled_destroy(bzr_tiled *plan);
  * packed share (the largest share, in whole tiles) -- each device sends 28 * npad bytes per frame. */
 bzr_status bzr_tiled_info(const bzr_tiled *plan, int32_t *transport, uint32_t *share_rays, uint32_t *npad);
 /* The frame's input rays [6][n] (host memory, or with BZR_DEVICE_PTRS ctxs[0]'s device memory) into every
- * device's share; synchronous.  They stay resident for every following frame. */
+ * device's share.  Waits for the frames in flight first (they read the previous rays).  The frame lands on
+ * device 0 once (host: one H2D copy, then the call waits for it so the host buffer may be reused; device:
+ * one D2D copy, which must find the source complete and unchanged until bzr_tiled_sync); device 0 extracts
+ * each device's share and sends it there (one peer copy per other device, (ndev - 1) / ndev of the frame
+ * in all), queued on ctxs[0]'s stream and ordered before the next bzr_tiled_trace without a host wait.
+ * With one device the frame is the share: one copy, nothing extracted.  The rays stay resident for every
+ * following frame. */
 bzr_status bzr_tiled_set_rays(bzr_tiled *plan, const float *rays_soa, uint32_t flags);
 /* Device d's share input [6][share_rays[d]] (device memory on device d), for callers that generate rays
  * on the devices: write it (ordered before the next bzr_tiled_trace, e.g. then bzr_tiled_sync). */
@@ -240,7 +248,8 @@ bzr_status bzr_tiled_share_rays(bzr_tiled *plan, uint32_t device_index, float **
  * out_status [n] and out_segments [n] (may be NULL) in input order.  BZR_DEVICE_PTRS: outputs on ctxs[0]'s
  * device; the call returns once the frame is queued (no host wait), frames on different slots overlap,
  * and the outputs are ready on bzr_tiled_stream's stream (or after bzr_tiled_sync) -- keep one set of
- * outputs per frame in flight.  Host pointers: synchronous.  Mode / pipeline flags pass through. */
+ * outputs per frame in flight.  Host pointers: synchronous, and a compact frame with more survivors than
+ * the capacity returns BZR_ERR_CAPACITY at once.  Mode / pipeline flags pass through. */
 bzr_status bzr_tiled_trace(bzr_tiled *plan, const bzr_mesh *const *lenses, const float *refractive_index,
                            uint32_t nlens, float *out_rays_soa, uint32_t *out_status, uint32_t *out_segments,
                            uint32_t flags);
@@ -253,7 +262,8 @@ bzr_status bzr_tiled_sync(bzr_tiled *plan);
  * share, npad columns) or BZR_PACK_COMPACT: one status/segment byte per ray, the survivor count and the
  * final rays of at most `cap` survivors (the rays that refracted at least once; 0 < cap <= npad) -- device
  * 0 returns the others' primary rays from its copy of the frame, so the compact layout needs
- * bzr_tiled_set_rays.  Synchronises first. */
+ * bzr_tiled_set_rays.  Synchronises first.  A BZR_GATHER_DIRECT plan gathers nothing: it keeps the layout,
+ * which has no effect on its frames. */
 bzr_status bzr_tiled_set_layout(bzr_tiled *plan, int32_t layout, uint32_t cap);
 /* Traces one frame (rays layout, synchronous), counts each device's survivors and switches to the compact
  * layout with cap = the largest count + 1/64 + 64 (at most npad); cap_out (may be NULL) gets it. */

@@ -39,6 +39,13 @@ for s in $STEPS; do
     prof)   step prof 1500 env TAG="${PROF_TAG:-prof}" BENCH="${PROF_BENCH:-}" WORKLOAD="${PROF_WORKLOAD:-}" \
               bash scripts/prof_run.sh ;;
     dropin) step dropin 400 bash scripts/dropin_latency.sh ;;
+    # the C++ host path (tests/cpp/tiled_bench.cpp: bzr::TiledChain frames on device outputs);
+    # CPPBENCH_ARGS e.g. "--host-frames 3"; appends its JSON line to cppbench.jsonl
+    cppbench) step cppbench_build 180 g++ -O2 -std=c++17 -ffp-contract=off -D__HIP_PLATFORM_AMD__ tests/cpp/tiled_bench.cpp \
+              -Iinclude/bzr -Iinclude -I/opt/rocm/include -Lcuda-bezier-triangle-raytracer_amd/lib -lbzr -L/opt/rocm/lib \
+              -lamdhip64 -Wl,-rpath,"$R/cuda-bezier-triangle-raytracer_amd/lib" -Wl,-rpath,/opt/rocm/lib -o /tmp/tiled_bench &&
+              step cppbench 300 /tmp/tiled_bench ${CPPBENCH_ARGS:-} &&
+              grep -h '^{' "$OUT/cppbench.log" >> "$OUT/cppbench.jsonl" ;;
     # bench lines of the other configs on both pipelines (bench defaults, 100 timed steps): configs.jsonl
     configs) for c in cfg5 cfg3 cfg2; do for p in staged fused; do
                step "configs_${c}_$p" 300 python bench.py --config $c --pipeline $p --steps 100 --cpu-baseline off &&

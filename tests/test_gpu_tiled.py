@@ -66,23 +66,27 @@ def test_tiled_device_pointers_equal_single_chain(bzr, ctx):
     _same(got, want)
 
 
-@pytest.mark.parametrize("transport,ndev", [("peer", 1), ("peer", 2), ("peer", 3), ("rccl", 1), ("auto", 1)])
+@pytest.mark.parametrize("transport,ndev", [("peer", 1), ("peer", 2), ("peer", 3), ("rccl", 1), ("auto", 1),
+                                           ("direct", 1), ("auto", 2)])
 def test_tiled_plan_frames_in_flight(bzr, ctx, transport, ndev):
     """A bzr_tiled plan over `ndev` list devices (all device 0 on this box: the peer path; the RCCL path is
-    the world-size-1 communicator with its self send/recv), 2 slots, 5 frames queued back to back with a
-    different refractive index per frame: each frame's device-0 outputs equal one bzr_trace_chain with
-    that index, so a slot buffer reused before its gather completed would fail."""
+    the world-size-1 communicator with its self send/recv; the one-device DIRECT path traces into the
+    outputs), 2 slots, 5 frames queued back to back with a different refractive index per frame: each
+    frame's device-0 outputs equal one bzr_trace_chain with that index, so a slot buffer reused before its
+    gather completed would fail."""
     import torch
 
     cfg, patches, _ = _cfg4(bzr)
     rays = grid_rays(cfg, side=256)
     n = rays.shape[1]
-    tp = {"peer": bzr.GATHER_PEER, "rccl": bzr.GATHER_RCCL, "auto": bzr.GATHER_AUTO}[transport]
+    tp = {"peer": bzr.GATHER_PEER, "rccl": bzr.GATHER_RCCL, "auto": bzr.GATHER_AUTO, "direct": bzr.GATHER_DIRECT}[transport]
     slots = [[bzr.Context(0) for _ in range(ndev)] for _ in range(2)]
     lenses = [[bzr.DeviceMesh(c, p) for p in patches] for c in slots[0]]  # device d's copy (same device here)
     plan = bzr.TiledPlan(slots, n, tile_rays=4096, transport=tp)
     got_tp, share, npad = plan.info()
-    assert got_tp == (bzr.GATHER_RCCL if transport in ("rccl", "auto") else bzr.GATHER_PEER)
+    # AUTO: DIRECT for one device; two list entries on one device are not distinct devices -> peer copies
+    assert got_tp == {"rccl": bzr.GATHER_RCCL, "peer": bzr.GATHER_PEER, "direct": bzr.GATHER_DIRECT,
+                      "auto": bzr.GATHER_DIRECT if ndev == 1 else bzr.GATHER_PEER}[transport]
     assert int(share.sum()) == n and npad == -(-16 // ndev) * 4096
     plan.set_rays(torch.from_numpy(rays).cuda())
     ris = [1.3, 1.45, 1.2, 1.6, 1.3]
@@ -133,7 +137,7 @@ def test_tiled_plan_share_rays_and_host_outputs(bzr, ctx):
     _same(out, bzr.trace_chain(ctx, [bzr.DeviceMesh(ctx, p) for p in patches], ri, rays))
 
 
-@pytest.mark.parametrize("transport,ndev", [("peer", 3), ("rccl", 1)])
+@pytest.mark.parametrize("transport,ndev", [("peer", 3), ("rccl", 1), ("direct", 1)])
 def test_tiled_plan_compact_gather(bzr, ctx, transport, ndev):
     """The compact layout (bzr_tiled_calibrate: one counted frame, then survivors only up to a capacity):
     frames bit-identical to one bzr_trace_chain, the rays that never refracted returned from device 0's copy
@@ -143,7 +147,7 @@ def test_tiled_plan_compact_gather(bzr, ctx, transport, ndev):
     cfg, patches, ri = _cfg4(bzr)
     rays = grid_rays(cfg, side=256)
     n = rays.shape[1]
-    tp = {"peer": bzr.GATHER_PEER, "rccl": bzr.GATHER_RCCL}[transport]
+    tp = {"peer": bzr.GATHER_PEER, "rccl": bzr.GATHER_RCCL, "direct": bzr.GATHER_DIRECT}[transport]
     slots = [[bzr.Context(0) for _ in range(ndev)] for _ in range(2)]
     lenses = [[bzr.DeviceMesh(c, p) for p in patches] for c in slots[0]]
     plan = bzr.TiledPlan(slots, n, tile_rays=4096, transport=tp)
@@ -164,12 +168,22 @@ def test_tiled_plan_compact_gather(bzr, ctx, transport, ndev):
     ho = (np.empty((6, n), np.float32), np.empty(n, np.uint32), np.empty(n, np.uint32))
     plan.trace(lenses, ri, *ho)
     _same(ho, want)
+    if transport == "direct":  # nothing is gathered: the capacity cannot be exceeded
+        plan.set_layout("compact", cap=64)
+        plan.trace(lenses, ri, *ho)
+        _same(ho, want)
+        plan.close()
+        return
     # too small a capacity: the frame is incomplete and sync says so
     plan.set_layout("compact", cap=64)
     plan.trace(lenses, ri, *outs[0])
     with pytest.raises(bzr.BzrError, match="capacity"):
         plan.sync()
     plan.sync()  # the flag was reported once
+    # ... and a synchronous host-output frame says so itself
+    with pytest.raises(bzr.BzrError, match="capacity"):
+        plan.trace(lenses, ri, *ho)
+    plan.sync()  # reported by the trace, not again here
     plan.close()
 
 
@@ -187,3 +201,61 @@ def test_tiled_plan_compact_needs_the_frame_rays(bzr, ctx):
     out = (np.empty((6, 8192), np.float32), np.empty(8192, np.uint32), np.empty(8192, np.uint32))
     with pytest.raises(bzr.BzrError, match="set_rays"):
         plan.trace(lenses, ri, *out)
+
+
+def test_tiled_plan_set_rays_waits_for_frames_in_flight(bzr, ctx):
+    """bzr_tiled_set_rays while frames are queued: the queued frames still see the old rays,
+    the frames after it the new ones -- on the DIRECT and the peer path."""
+    import torch
+
+    cfg, patches, ri = _cfg4(bzr)
+    rays_a = grid_rays(cfg, side=256)
+    rays_b = rays_a.copy()
+    rays_b[2] += np.float32(0.37)  # shifted image: different hits
+    n = rays_a.shape[1]
+    single = [bzr.DeviceMesh(ctx, p) for p in patches]
+    want_a, want_b = bzr.trace_chain(ctx, single, ri, rays_a), bzr.trace_chain(ctx, single, ri, rays_b)
+    for tp, ndev in ((bzr.GATHER_DIRECT, 1), (bzr.GATHER_PEER, 2)):
+        slots = [[bzr.Context(0) for _ in range(ndev)] for _ in range(3)]
+        lenses = [[bzr.DeviceMesh(c, p) for p in patches] for c in slots[0]]
+        plan = bzr.TiledPlan(slots, n, tile_rays=4096, transport=tp)
+        outs = [(torch.empty((6, n), device="cuda"), torch.empty(n, dtype=torch.int32, device="cuda"),
+                 torch.empty(n, dtype=torch.int32, device="cuda")) for _ in range(6)]
+        plan.set_rays(torch.from_numpy(rays_a).cuda())
+        for o in outs[:3]:
+            plan.trace(lenses, ri, *o)
+        plan.set_rays(rays_b)  # host rays this time
+        for o in outs[3:]:
+            plan.trace(lenses, ri, *o)
+        plan.sync()
+        for o in outs[:3]:
+            _same(o, want_a)
+        for o in outs[3:]:
+            _same(o, want_b)
+        plan.close()
+
+
+def test_tiled_plan_distinct_devices(bzr, ctx):
+    """Two distinct HIP devices (the peer path's events live on the device of the stream that
+    records them): the peer and RCCL transports, bit-identical to one bzr_trace_chain.  Needs two GPUs."""
+    import torch
+
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs two GPUs (the GPU box has one)")
+    cfg, patches, ri = _cfg4(bzr)
+    rays = grid_rays(cfg, side=256)
+    n = rays.shape[1]
+    want = bzr.trace_chain(ctx, [bzr.DeviceMesh(ctx, p) for p in patches], ri, rays)
+    for tp in (bzr.GATHER_PEER, bzr.GATHER_RCCL):
+        slots = [[bzr.Context(0), bzr.Context(1)] for _ in range(2)]
+        lenses = [[bzr.DeviceMesh(c, p) for p in patches] for c in slots[0]]
+        plan = bzr.TiledPlan(slots, n, tile_rays=4096, transport=tp)
+        plan.set_rays(torch.from_numpy(rays).cuda())
+        outs = [(torch.empty((6, n), device="cuda:0"), torch.empty(n, dtype=torch.int32, device="cuda:0"),
+                 torch.empty(n, dtype=torch.int32, device="cuda:0")) for _ in range(3)]
+        for o in outs:
+            plan.trace(lenses, ri, *o)
+        plan.sync()
+        for o in outs:
+            _same(o, want)
+        plan.close()
