@@ -228,6 +228,105 @@ def pmc_traffic(kernel, workload):
     return round(total), f"{d['source']} ({d['method']})"
 
 
+GOLDEN = REPO / "tests" / "golden"
+
+
+def oracle_digests(cfg, side, rays_img, status_img, seg_img):
+    """The whole frame (row-major full-image arrays) against the committed oracle digests of this workload
+    (tests/golden/d_<cfg>_<side>.npz: one SHA-256 per 64x64 tile, made by tests/golden/make_digests.py from the
+    CPU oracle -- data, not the oracle).  None when no digests exist for it."""
+    import importlib.util
+
+    path = GOLDEN / f"d_{cfg.name}_{side}.npz"
+    if not path.exists() or cfg.op != "chain":
+        return None
+    spec = importlib.util.spec_from_file_location("tile_digest", GOLDEN / "tile_digest.py")
+    td = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(td)
+    g = np.load(path)
+    rows, cols = td.tile_pixels(cfg, side, g["tiles"])
+    flat = rows * side + cols
+    got = td.chain_digests(rays_img[:, flat], status_img[flat], seg_img[flat])
+    match = int((got == g["digests"]).all(axis=1).sum())
+    return {"tiles_matching": match, "tiles": int(len(g["tiles"])), "ok": match == len(g["tiles"]),
+            "source": str(path.relative_to(REPO))}
+
+
+def verify_frame(a, cfg, chain, world, rank, side, height, ctx, meshes, ris, mode, dev, gather, loop, last, own_out, cap):
+    """Untimed checks of what the timed frames delivered.  Returns {"gather": {...} (N > 1), "frame": {...}}.
+    N > 1: rank 0 traces the whole image itself and compares the last gathered frame with it bit for bit
+    (frame.verify_gathered), then that frame with the oracle digests; all ranks time the gather alone.
+    N = 1: the last frame's own outputs against the oracle digests."""
+    import torch
+    import torch.distributed as dist
+
+    from bzr_amd import frame
+    import bzr_amd
+
+    out = {"gather": {}, "frame": None}
+    total = side * height
+    host_bytes = total * (32 if chain else 52) * 3  # reference image + assembled image + temporaries
+    if rank == 0:
+        if host_bytes > 24e9:
+            msg = f"skipped: {total} pixels ({host_bytes / 1e9:.0f} GB of host arrays)"
+            out["frame"] = {"skipped": msg}
+            if gather:
+                out["gather"]["gather_verified"] = None
+                out["gather"]["gather_verify"] = {"skipped": msg}
+        elif world == 1:
+            if chain:
+                rows, cols, _ = frame.rank_rays(cfg, 0, 1, side, height)
+                flat = rows * side + cols
+                r, s_, g_ = (t.cpu().numpy() for t in own_out)
+                img = np.zeros((6, total), np.float32), np.zeros(total, np.uint32), np.zeros(total, np.uint32)
+                img[0][:, flat], img[1][flat], img[2][flat] = r, s_.view(np.uint32), g_.view(np.uint32)
+                out["frame"] = {"oracle_digests": oracle_digests(cfg, side, *img), "what": "the last timed frame"}
+        else:
+            rows, cols, rays_all = frame.rank_rays(cfg, 0, 1, side, height)  # every tile, in one process
+            flat = rows * side + cols
+            rt = torch.from_numpy(rays_all).to(dev)
+            m = rays_all.shape[1]
+            if chain:
+                o = (torch.empty((6, m), dtype=torch.float32, device=dev), torch.empty(m, dtype=torch.int32, device=dev),
+                     torch.empty(m, dtype=torch.int32, device=dev))
+                bzr_amd.trace_chain(ctx, meshes, ris, rt, *o, mode=mode)
+                torch.cuda.synchronize()
+                want = {"rays": np.zeros((6, total), np.float32), "status": np.zeros(total, np.uint32),
+                        "segments": np.zeros(total, np.uint32)}
+                want["rays"][:, flat] = o[0].cpu().numpy()
+                want["status"][flat] = o[1].cpu().numpy().view(np.uint32)
+                want["segments"][flat] = o[2].cpu().numpy().view(np.uint32)
+            else:
+                h = torch.empty((13, m), dtype=torch.float32, device=dev)
+                bzr_amd.intersect(ctx, meshes[0], rt, h, mode=mode)
+                torch.cuda.synchronize()
+                want = {"hits": np.zeros((13, total), np.float32)}
+                want["hits"][:, flat] = h.cpu().numpy()
+            del rt
+            if gather and "parts" in last:
+                res = frame.verify_gathered(last["parts"], a.gather, cfg, world, side, height, want, cap=cap)
+                out["gather"]["gather_verified"] = res["ok"]
+                out["gather"]["gather_verify"] = dict(res, frame_index=last["frame"],
+                                                      against="the same frame traced by rank 0 in one process")
+            if chain:
+                out["frame"] = {"oracle_digests": oracle_digests(cfg, side, want["rays"], want["status"], want["segments"]),
+                                "what": "rank 0's single-process trace of the whole image (the gathered frame's reference)"}
+    if gather:  # the gather alone: K gathers of the packed buffers back to back (no tracing), max over ranks
+        kk = max(5, min(a.steps, 20))
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(kk):
+            w = frame.gather(loop.packed[k % 2], world, rank, gather_list=loop.lists[k % 2], async_op=True)
+            w.wait()
+        torch.cuda.synchronize()
+        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        out["gather"]["gather_only_ms_per_frame"] = round(float(t[0]) / kk * 1e3, 4)
+        out["gather"]["gather_only_frames"] = kk
+    return out
+
+
 def main():
     a = parse()
     from bzr_amd import launch  # no torch, no HIP: safe in the launching parent
@@ -364,8 +463,10 @@ def main():
     else:
         pack_fn = ((lambda out, p, f: p[0, :n].copy_(out[11])) if a.gather == "image" else
                    (lambda out, p, f: p[:, :n].copy_(out)))
+    last_gathered = {}  # rank 0: the latest frame's gathered parts (kept by reference; checked after the timed region)
     loop = frame.FrameLoop(world, rank, n, npad, a.gather, trace, outs, stream_for=lambda f: torch.cuda.stream(streams[f]),
-                           cap=cap, device=dev, pack_fn=pack_fn, rows=0 if chain else 13)
+                           cap=cap, device=dev, pack_fn=pack_fn, rows=0 if chain else 13,
+                           on_gathered=lambda k, parts: last_gathered.update(frame=k, parts=parts))
 
     def step(inflight=F):
         loop.step(inflight)
@@ -418,6 +519,12 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t_start
     chain_ms = events[0].elapsed_time(events[1]) / a.steps
+    last_slot = (loop.frames - 1) % F  # the slot of the last timed frame (its outputs are still in place)
+    # What the timed frames delivered (untimed): rank 0 checks the last gathered frame
+    # against the same frame traced in one process, and (cfg4 4096^2) that frame against the committed oracle
+    # digests; at N = 1 the last frame's own outputs against the digests.  Then the gather alone, timed.
+    verify = verify_frame(a, cfg, chain, world, rank, side, height, ctx, meshes, ris, mode, dev, gather, loop,
+                          last_gathered, outs[last_slot], cap)
     # per-kernel HIP-event timing on the kernels' stream, in a separate untimed pass of the same
     # K steps (the per-launch events would otherwise sit inside the timed region)
     ctx.timing(True)
@@ -531,8 +638,10 @@ def main():
                                + (f", RCCL gather of every frame to rank 0 (overlapped with the next frames): "
                                   f"{loop.bytes_per_rank / npad:.2f} B per primary ({a.gather})" if gather else ""),
                 "gather": ({"layout": a.gather, "bytes_per_rank_per_frame": loop.bytes_per_rank,
-                            "bytes_per_primary": round(loop.bytes_per_rank / npad, 3), "compact_capacity": cap or None}
+                            "bytes_per_primary": round(loop.bytes_per_rank / npad, 3), "compact_capacity": cap or None,
+                            **verify["gather"]}
                            if gather else None),
+                "frame_verified": verify["frame"],
                 "pipeline": a.pipeline,
                 "frames_in_flight": F,
                 "hw_queues": {"GPU_MAX_HW_QUEUES_requested": hwq, "source": hwq_source,

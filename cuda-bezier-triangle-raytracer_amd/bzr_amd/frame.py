@@ -100,6 +100,62 @@ def assemble(parts, cfg: Config, world: int, width: int, height: int, cap: int =
     return rays, status, seg
 
 
+def assemble_hits(parts, cfg: Config, world: int, width: int, height: int):
+    """Rank 0, intersect configs: the gathered parts -> the full image's BezierIntersection rows, row-major
+    pixels: hits [13, height*width] (the rays layout, 13 rows per rank) or, for the image layout (one row: the
+    hit's `what` word), what [height*width] uint32."""
+    out = None
+    for r, part in enumerate(parts):
+        p = part.cpu().numpy() if hasattr(part, "cpu") else np.asarray(part)
+        rows, cols = shard_pixels(cfg, r, world, side=width, height=height, block=TILE)
+        flat = rows * width + cols
+        p = np.ascontiguousarray(p[:, :len(flat)]).view(np.uint32)
+        if out is None:
+            out = np.zeros((p.shape[0], height * width), np.uint32)
+        out[:, flat] = p
+    return out if out.shape[0] > 1 else out[0]
+
+
+def verify_gathered(parts, layout: str, cfg: Config, world: int, width: int, height: int, want: dict, cap: int = 0):
+    """Rank 0: one gathered frame against `want`, the same frame traced in one process (full-image arrays in
+    row-major pixel order: chain configs "rays" [6, HW], "status", "segments"; intersect configs "hits"
+    [13, HW]).  Bit-for-bit on every word the layout carries (the image layout: the status / segment word, or
+    the hit's `what`; compact and rays: the final rays too).  Returns {"ok", "mismatched_pixels", "compared",
+    "survivors_max" (compact: the largest rank's survivor count word), "cap", "error"}; a compact part whose
+    survivors exceed the capacity or disagree with its count word fails with that error."""
+    res = {"ok": False, "mismatched_pixels": None, "compared": None, "survivors_max": None,
+           "cap": cap if layout == "compact" else None, "error": None}
+    if layout == "compact":
+        nw = compact_words(padded_count(world, width, height))
+        res["survivors_max"] = max(int(np.ascontiguousarray((p.cpu().numpy() if hasattr(p, "cpu") else np.asarray(p))
+                                                           [nw:nw + 1]).view(np.int32)[0]) for p in parts)
+    bad = np.zeros(height * width, bool)
+    try:
+        if "hits" in want:
+            got = assemble_hits(parts, cfg, world, width, height)
+            ref = np.ascontiguousarray(want["hits"]).view(np.uint32)
+            if got.ndim == 1:
+                bad |= got != ref[11]
+                res["compared"] = ["what"]
+            else:
+                bad |= (got != ref).any(axis=0)
+                res["compared"] = ["hits[13]"]
+        else:
+            rays, status, seg = assemble(parts, cfg, world, width, height, cap=cap)
+            bad |= status != np.asarray(want["status"], np.uint32)
+            bad |= seg != np.asarray(want["segments"], np.uint32)
+            res["compared"] = ["status", "segments"]
+            if rays is not None:
+                bad |= (rays.view(np.uint32) != np.ascontiguousarray(want["rays"]).view(np.uint32)).any(axis=0)
+                res["compared"].append("rays[6]")
+    except RuntimeError as e:  # compact capacity / count mismatch (unpack_compact)
+        res["error"] = str(e)
+        return res
+    res["mismatched_pixels"] = int(bad.sum())
+    res["ok"] = res["mismatched_pixels"] == 0
+    return res
+
+
 # ------------------------------------------------------------------ compact layout
 def compact_words(npad: int) -> int:
     """int32 words holding one status/segments byte per primary (npad is a multiple of 4096)."""

@@ -190,3 +190,58 @@ def test_compact_capacity_overflow_is_reported():
     r, st, sg = frame.unpack_compact(packed, n, npad, cap, np.zeros((6, n), np.float32))
     assert np.array_equal(r[:, 100:], rays.numpy()[:, 100:]) and (r[:, :100] == 0).all()
     assert np.array_equal(sg, seg.numpy().astype(np.uint32))
+
+
+@pytest.mark.parametrize("layout", ["compact", "rays", "image"])
+def test_verify_gathered_accepts_the_frame_and_rejects_a_corrupted_part(bzr, orc, layout):
+    """bench.py's multi-rank check (frame.verify_gathered): rank 0 compares the gathered
+    parts with the same frame traced in one process.  Two ranks' parts packed from the oracle's trace pass;
+    one flipped bit in one part, or a compact count word that disagrees with the flagged survivors, fails."""
+    import torch
+
+    cfg = CONFIGS["cfg2"]
+    patches = bzr.TriMesh().make_ellipsoid(32, 16, (1, 4, 2)).translate((10, 0, 0)).standardize().bezier_patches()
+    world, width, height = 2, 128, 128
+    npad = frame.padded_count(world, width, height)
+    per_rank = []
+    for r in range(world):
+        _, _, rays = frame.rank_rays(cfg, r, world, width, height)
+        per_rank.append(orc.trace_chain([patches], [1.3], rays, threads=2))
+    cap = frame.compact_capacity(max(int(frame.survivors(s, g).sum()) for _, s, g in per_rank), npad)
+    parts = []
+    for o, s, g in per_rank:
+        to = (torch.from_numpy(o), torch.from_numpy(s.view(np.int32)), torch.from_numpy(g.view(np.int32)))
+        if layout == "compact":
+            p = torch.zeros(frame.compact_size(npad, cap))
+            frame.pack_compact(to[1], to[2], to[0], p, npad, cap)
+        else:
+            p = torch.zeros((frame.PACKED_ROWS if layout == "rays" else frame.IMAGE_ROWS, npad))
+            frame.pack(*to, p)
+        parts.append(p)
+    rows, cols, rays = frame.rank_rays(cfg, 0, 1, width, height)
+    o, s, g = orc.trace_chain([patches], [1.3], rays, threads=2)
+    flat = rows * width + cols
+    want = {"rays": np.zeros((6, width * height), np.float32), "status": np.zeros(width * height, np.uint32),
+            "segments": np.zeros(width * height, np.uint32)}
+    want["rays"][:, flat], want["status"][flat], want["segments"][flat] = o, s, g
+    res = frame.verify_gathered(parts, layout, cfg, world, width, height, want, cap=cap)
+    assert res["ok"] and res["mismatched_pixels"] == 0, res
+    assert ("rays[6]" in res["compared"]) == (layout != "image")
+    if layout == "compact":
+        assert 0 < res["survivors_max"] <= cap
+    bad = [p.clone() for p in parts]
+    if layout == "image":  # a segment count off by one in rank 1's word row
+        w = bad[1][0].view(torch.int32)
+        w[5] += 1 << 8
+    elif layout == "rays":
+        bad[1][2, 7] = torch.nextafter(bad[1][2, 7], torch.tensor(1e30))
+    else:  # a survivor's ray, then the count word
+        nw = frame.compact_words(npad)
+        bad[1][nw + 1 + 3] = torch.nextafter(bad[1][nw + 1 + 3], torch.tensor(1e30))
+    res = frame.verify_gathered(bad, layout, cfg, world, width, height, want, cap=cap)
+    assert not res["ok"] and res["mismatched_pixels"] == 1, res
+    if layout == "compact":
+        bad = [p.clone() for p in parts]
+        bad[0][nw:nw + 1].view(torch.int32)[0] -= 1
+        res = frame.verify_gathered(bad, layout, cfg, world, width, height, want, cap=cap)
+        assert not res["ok"] and "not fully gathered" in res["error"]
