@@ -554,6 +554,7 @@ def main():
         newton_runs = work_cnt["pairs"] + work_cnt["follows"]
         exec_flops = FLOPS_NEWTON * newton_runs + FLOPS_PLANAR * work_cnt["gate_tests"] + FLOPS_REFRACT * segs
         bf_flops = FLOPS_PLANAR * n_patch / len(patches) * segs + FLOPS_NEWTON * newton_runs + FLOPS_REFRACT * segs
+        fused_kernel = "k_trace" in kernels
         if "k_newton_lane" in kernels and "k_newton" in kernels:
             (m1, c1), (m2, _) = kernels.pop("k_newton"), kernels.pop("k_newton_lane")
             kernels["k_newton+k_newton_lane"] = (m1 + m2, c1)
@@ -674,8 +675,14 @@ def main():
                     "gate_tests": round(work_cnt["gate_tests"] / segs, 4),
                     "node_visits_per_wave_segment": round(work_cnt["node_visits"] * 64 / segs, 3),
                     "leaf_fetches_per_wave_segment": round(work_cnt["leaf_fetches"] * 64 / segs, 3),
-                    "newton_lane_utilisation": round(newton_runs / max(1, 64 * work_cnt["newton_rounds"]), 4)
+                    # fused: every Newton run (cThis pairs + follow-side retries) happens in k_trace's patch-uniform
+                    # passes; staged: the passes are k_newton's / k_newton_lane's 64-pair chunks, which hold the
+                    # candidate pairs only (the retries run per lane in k_resolve), so pairs / (64 x chunks)
+                    "newton_lane_utilisation": round((newton_runs if fused_kernel else work_cnt["pairs"])
+                                                     / max(1, 64 * work_cnt["newton_rounds"]), 4)
                     if work_cnt["newton_rounds"] else None,
+                    "newton_lane_utilisation_def": ("(pairs + follow retries) / (64 x k_trace passes)" if fused_kernel
+                                                    else "pairs / (64 x k_newton + k_newton_lane chunks)"),
                     "overflow_rays_per_frame": work_cnt["overflow_rays"],
                     "source": "GPU counters (bzr_ctx_counters), rank 0, one frame",
                     "oracle_sample_rates": ({"newton": round(cnt["newton"] / cnt["segments"], 4),

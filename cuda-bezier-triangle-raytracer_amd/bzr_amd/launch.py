@@ -17,6 +17,7 @@ import signal
 import socket
 import subprocess
 import sys
+import threading
 import time
 
 LAUNCHED_BY = "BZR_LAUNCHED_BY"  # set in the children's environment: "bench.py" (self-launched)
@@ -69,20 +70,44 @@ def spawn(argv: list[str], n: int, env=None, master_addr: str = "127.0.0.1", pol
         raise
     status, failed_at = 0, None
     live = set(range(n))
-    while live:
-        for r in sorted(live):
-            rc = procs[r].poll()
-            if rc is None:
-                continue
-            live.discard(r)
-            if rc != 0 and status == 0:
-                status = rc if rc > 0 else 128 - rc
-                failed_at = time.monotonic()
-                print(f"bench.py: rank {r} exited with status {rc}; stopping the other ranks", file=sys.stderr, flush=True)
+
+    def on_term(signum, frame):  # a SIGTERM to the parent unwinds through the finally below
+        raise SystemExit(128 + signum)
+
+    old_term = signal.signal(signal.SIGTERM, on_term) if threading.current_thread() is threading.main_thread() else None
+    try:
+        while live:
+            for r in sorted(live):
+                rc = procs[r].poll()
+                if rc is None:
+                    continue
+                live.discard(r)
+                if rc != 0 and status == 0:
+                    status = rc if rc > 0 else 128 - rc
+                    failed_at = time.monotonic()
+                    print(f"bench.py: rank {r} exited with status {rc}; stopping the other ranks", file=sys.stderr, flush=True)
+                    for q in live:
+                        procs[q].send_signal(signal.SIGTERM)
+            if failed_at is not None and live and time.monotonic() - failed_at > 15.0:
                 for q in live:
-                    procs[q].send_signal(signal.SIGTERM)
-        if failed_at is not None and live and time.monotonic() - failed_at > 15.0:
-            for q in live:
-                procs[q].kill()
-        time.sleep(poll_s)
+                    procs[q].kill()
+            time.sleep(poll_s)
+    finally:  # the parent interrupted (KeyboardInterrupt, SIGTERM): no rank outlives it
+        _stop([procs[q] for q in live])
+        if old_term is not None:
+            signal.signal(signal.SIGTERM, old_term)
     return status
+
+
+def _stop(procs, grace_s: float = 15.0):
+    """SIGTERM the running children, SIGKILL those still running after `grace_s`, and reap them."""
+    running = [p for p in procs if p.poll() is None]
+    for p in running:
+        p.send_signal(signal.SIGTERM)
+    deadline = time.monotonic() + grace_s
+    for p in running:
+        try:
+            p.wait(timeout=max(0.0, deadline - time.monotonic()))
+        except subprocess.TimeoutExpired:
+            p.kill()
+            p.wait()

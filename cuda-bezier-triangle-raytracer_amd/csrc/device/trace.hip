@@ -2442,12 +2442,13 @@ bool use_fast(uint32_t flags) { return (flags & BZR_MODE_FAST) != 0; }
 // rays per patch stands in for how many patches a wave's 64 rays meet).  Chosen for callers that keep
 // frames in flight (bench.py): cfg4 at 4096^2 (5461 rays per patch) and cfg2 at 1024^2
 // (341) run fused -- cfg2 5593 vs 5205 Mrays/s at three / two frames in flight, though a lone cfg2 frame
-// is faster staged; cfg3 (145) and cfg5 (223) run staged.
+// is faster staged; cfg3 (145) and cfg5 (223) run staged.  Meshes of kStagedPatchLimit patches or more
+// (the staged key and pair encoding's limit) always run fused, which takes any mesh.
 constexpr uint64_t kFusedRaysPerPatch = 256;
 bool use_staged(uint32_t flags, uint64_t n, uint64_t nb) {
   if (flags & BZR_PIPELINE_STAGED) return true;
   if (flags & BZR_PIPELINE_FUSED) return false;
-  return n < kFusedRaysPerPatch * nb;
+  return nb < kStagedPatchLimit && n < kFusedRaysPerPatch * nb;
 }
 // BZR_MODE_FAST runs on the culled pipeline's kernels only; the brute-force scan is the parity reference.
 constexpr uint32_t kKnownFlags = BZR_DEVICE_PTRS | BZR_MODE_FAST | BZR_ACCEL_NONE | BZR_PIPELINE_STAGED | BZR_PIPELINE_FUSED;
@@ -2595,7 +2596,9 @@ bzr_status run_culled(bzr_ctx *ctx, const MeshView &mv, const float *rays, uint3
   const uint32_t nb = mv.n;
   const uint32_t hn = nb;
   const bool small_scan = hn + 1 <= kScanSmall;
-  if (nb >= kStagedPatchLimit) return BZR_ERR_INVALID_ARGUMENT;  // (the fused path takes any mesh)
+  if (nb >= kStagedPatchLimit)  // (the automatic choice sends such meshes to the fused path, which takes any mesh)
+    return set_error(BZR_ERR_INVALID_ARGUMENT, "staged path: mesh of " + std::to_string(nb) +
+                                                   " patches, at or above 2^25; use BZR_PIPELINE_FUSED");
   if (!(ctx->zero_ctr == w.ctr && ctx->zero_hn >= hn))  // counters + histogram [0, hn] to zero
     BZR_HIP(hipMemsetAsync(w.ctr, 0, reinterpret_cast<char *>(w.hist + hn + 1) - reinterpret_cast<char *>(w.ctr),
                            ctx->stream));

@@ -79,10 +79,16 @@ enum {
   /* Culled-path pipeline (same output bits either way; neither flag = automatic choice):
    *   fused   one kernel per call (k_trace): each wave walks the BVH and runs the Newton stage for its own
    *           rays with patch-uniform records -- no per-pair HBM traffic; best when a wave's rays meet
-   *           few distinct patches (dense ray grids: more than ~2000 rays per patch)
+   *           few distinct patches (dense ray grids, many rays per patch)
    *   staged  traverse -> bucket pairs by patch -> Newton -> resolve -> finish per segment; full-wave
-   *           Newton passes whatever the ray coherence, at ~12x the algorithmic HBM bytes
-   * automatic: fused when n >= 256 x the largest lens's patch count, else staged. */
+   *           Newton passes whatever the ray coherence, at 3-12x the algorithmic HBM bytes
+   * automatic: fused when n >= 256 x the largest lens's patch count (and always for meshes of 2^25 patches
+   * or more, which the staged encoding cannot hold), else staged.  The 256 is tuned for callers that keep
+   * two or three frames in flight (bench.py, bzr_tiled with several slots): there the fused path wins from
+   * ~256 rays per patch up.  A caller that traces ONE frame at a time and waits for it sees the fused
+   * frame's tail (its slowest waves, ~0.3-0.5 ms) undiluted; for such callers the staged path wins up to
+   * ~2000 rays per patch (cfg2, 341 rays per patch: staged 3 859 vs fused 2 916 Mrays/s on lone frames),
+   * so pass BZR_PIPELINE_STAGED explicitly there (DESIGN.md (a) "Which one runs"). */
   BZR_PIPELINE_STAGED = 8u,
   BZR_PIPELINE_FUSED = 16u
 };

@@ -88,3 +88,30 @@ def test_spawn_stops_the_others_when_a_rank_dies_early(tmp_path):
                         f"from bzr_amd import launch; sys.exit(launch.spawn([sys.executable, {str(script)!r}], 2))"],
                        capture_output=True, text=True, timeout=60)
     assert r.returncode == 5, r.stderr
+
+
+def test_parent_sigterm_stops_the_ranks(tmp_path):
+    """a SIGTERM to the launching parent while it waits stops every rank (SIGTERM, then
+    SIGKILL after the grace period) instead of leaving them running on the GPUs."""
+    import signal
+    import time
+
+    pids = tmp_path / "pids"
+    pids.mkdir()
+    child = f"import os, time; open(os.path.join({str(pids)!r}, os.environ['RANK']), 'w').write(str(os.getpid())); time.sleep(120)"
+    parent = (f"import sys; sys.path.insert(0, {str(REPO / 'cuda-bezier-triangle-raytracer_amd')!r}); "
+              f"from bzr_amd import launch; sys.exit(launch.spawn([sys.executable, '-c', {child!r}], 2))")
+    p = subprocess.Popen([sys.executable, "-c", parent])
+    try:
+        deadline = time.monotonic() + 60
+        while len(list(pids.iterdir())) < 2 and time.monotonic() < deadline:
+            time.sleep(0.1)
+        ranks = [int((pids / str(r)).read_text()) for r in range(2)]
+        p.send_signal(signal.SIGTERM)
+        assert p.wait(timeout=60) == 128 + signal.SIGTERM
+        for pid in ranks:  # reaped by the parent: no such process any more
+            with pytest.raises(ProcessLookupError):
+                os.kill(pid, 0)
+    finally:
+        if p.poll() is None:
+            p.kill()
