@@ -412,7 +412,8 @@ extern "C" bzr_status bzr_tiled_create(bzr_ctx *const *ctxs, uint32_t ndev, uint
   if (!ctxs || ndev == 0 || nslot == 0) return fail(BZR_ERR_INVALID_ARGUMENT, "bzr_tiled_create: no contexts");
   if (tile_rays == 0) return fail(BZR_ERR_INVALID_ARGUMENT, "bzr_tiled_create: tile_rays must be > 0");
   if (n == 0) return fail(BZR_ERR_INVALID_ARGUMENT, "bzr_tiled_create: empty frame");
-  if (transport != BZR_GATHER_AUTO && transport != BZR_GATHER_RCCL && transport != BZR_GATHER_PEER)
+  if (transport != BZR_GATHER_AUTO && transport != BZR_GATHER_RCCL && transport != BZR_GATHER_PEER &&
+      transport != BZR_GATHER_DIRECT)
     return fail(BZR_ERR_INVALID_ARGUMENT, "bzr_tiled_create: unknown transport " + std::to_string(transport));
   const size_t nctx = (size_t)ndev * nslot;
   for (size_t k = 0; k < nctx; ++k)
