@@ -38,4 +38,10 @@ struct bzr_ctx {
   bool wave_clock_real = false;  // bzr_debug_wave_clock_rate: also s_memrealtime (4 words per wave)
   void *pack = nullptr;     // bzr_pack_frame: per-block survivor counts and offsets (compact layout)
   size_t pack_bytes = 0;
+  // cost-ordered k_trace dispatch (trace.hip run_fused): each wave of a fused call writes its cost class;
+  // three small kernels turn them into a longest-first order of the waves, which the next fused call of the
+  // same size dispatches in.  sched: device [cap] cost bins | [cap] order | histogram | offsets.
+  uint32_t *sched = nullptr;
+  uint32_t sched_cap = 0;    // waves the buffer holds
+  uint32_t sched_waves = 0;  // waves of the call whose order is ready (0: none)
 };

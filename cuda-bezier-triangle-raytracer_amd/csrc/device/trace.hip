@@ -2183,6 +2183,8 @@ struct TraceJob {
   uint32_t ld;               // row stride of rays / out_rays / hits (>= n)
   unsigned long long *wave_clock;  // optional test hook: [2 * waves] start, duration (s_memtime ticks)
   uint32_t wave_real;              // wave_clock holds [4 * waves]: + s_memrealtime start, duration (100 MHz)
+  const uint32_t *order;           // optional: block b traces tile order[b] (cost-ordered dispatch, run_fused)
+  uint32_t *cost;                  // optional: per tile, its cost bin (sched_bin of the block's duration)
 };
 
 // BZR_TRACE_WPE (default 6): amdgpu_waves_per_eu lower bound for k_trace.  The chain kernel needs 72 VGPRs
@@ -2218,14 +2220,75 @@ constexpr int kTraceBlock = BZR_TRACE_BLOCK, kTraceWaves = kTraceBlock / 64;
 __device__ __forceinline__ uint32_t trace_tile(uint32_t b, uint32_t nblocks) {
   return deal_blocks<BZR_TRACE_XCD>(b, nblocks);
 }
+// Cost-ordered dispatch (BZR_TRACE_SCHED, default on).  A frame's waves differ up to ~6x
+// in duration (rim waves meet many patches), and the hardware dispatches blocks in index order as slots free
+// up -- greedy list scheduling.  One frame alone therefore ends on whichever long waves were dispatched late.
+// Each k_trace block records its duration's cost bin; k_sched_* order the tiles longest-first (a counting
+// sort over kSchedBins classes, 4 per octave of cycles), and the context's next fused call of the same size
+// dispatches in that order: longest-processing-time-first list scheduling.  Every tile is traced exactly
+// once either way and waves share nothing, so the output bits do not depend on the order.
+#ifndef BZR_TRACE_SCHED
+#define BZR_TRACE_SCHED 1
+#endif
+constexpr uint32_t kSchedBins = 128, kSchedMinTiles = 2048, kSchedThreads = 256;
+__device__ __forceinline__ uint32_t sched_bin(unsigned long long cycles) {
+  const uint32_t c = static_cast<uint32_t>(cycles > 0xFFFFFFFFull ? 0xFFFFFFFFull : cycles) | 4u;
+  const uint32_t lg = 31u - __clz(c);                           // >= 2
+  const uint32_t key = 4u * lg + ((c >> (lg - 2u)) & 3u);       // 4 classes per octave, 8..127
+  return kSchedBins - 1u - key;                                  // bin 0 = the longest
+}
+// tiles per bin (hist zeroed by the previous k_sched_scan, or at allocation)
+__global__ __launch_bounds__(kSchedThreads) void k_sched_count(const uint32_t *__restrict__ bin, uint32_t tiles,
+                                                               uint32_t *__restrict__ hist) {
+  __shared__ uint32_t h[kSchedBins];
+  for (uint32_t k = threadIdx.x; k < kSchedBins; k += kSchedThreads) h[k] = 0u;
+  __syncthreads();
+  const uint32_t t = blockIdx.x * kSchedThreads + threadIdx.x;
+  if (t < tiles) atomicAdd(&h[bin[t] & (kSchedBins - 1u)], 1u);
+  __syncthreads();
+  for (uint32_t k = threadIdx.x; k < kSchedBins; k += kSchedThreads)
+    if (h[k]) atomicAdd(&hist[k], h[k]);
+}
+// offs = exclusive scan of hist; hist back to zero for the next count
+__global__ __launch_bounds__(kSchedBins) void k_sched_scan(uint32_t *__restrict__ hist, uint32_t *__restrict__ offs) {
+  __shared__ uint32_t v[kSchedBins];
+  const uint32_t k = threadIdx.x;
+  const uint32_t mine = hist[k];
+  v[k] = mine;
+  __syncthreads();
+  for (uint32_t s = 1; s < kSchedBins; s <<= 1) {
+    const uint32_t a = k >= s ? v[k - s] : 0u;
+    __syncthreads();
+    v[k] += a;
+    __syncthreads();
+  }
+  offs[k] = v[k] - mine;
+  hist[k] = 0u;
+}
+// order[offs[bin] + rank within the bin] = tile (block-aggregated reservations)
+__global__ __launch_bounds__(kSchedThreads) void k_sched_place(const uint32_t *__restrict__ bin, uint32_t tiles,
+                                                               uint32_t *__restrict__ offs, uint32_t *__restrict__ order) {
+  __shared__ uint32_t h[kSchedBins], base[kSchedBins];
+  for (uint32_t k = threadIdx.x; k < kSchedBins; k += kSchedThreads) h[k] = 0u;
+  __syncthreads();
+  const uint32_t t = blockIdx.x * kSchedThreads + threadIdx.x;
+  const uint32_t b = t < tiles ? (bin[t] & (kSchedBins - 1u)) : 0u;
+  const uint32_t r = t < tiles ? atomicAdd(&h[b], 1u) : 0u;
+  __syncthreads();
+  for (uint32_t k = threadIdx.x; k < kSchedBins; k += kSchedThreads)
+    base[k] = h[k] ? atomicAdd(&offs[k], h[k]) : 0u;
+  __syncthreads();
+  if (t < tiles) order[base[b] + r] = t;
+}
 template <int kMode, bool kFast, bool kCount>
 __global__ __launch_bounds__(kTraceBlock) BZR_TRACE_ATTR void k_trace(LensSet lenses, TraceJob job,
                                                                       unsigned long long *__restrict__ counters) {
   __shared__ TraceLds<kMode> lds[kTraceWaves];
   const uint32_t lane = threadIdx.x & 63u;
   TraceLds<kMode> &L = lds[threadIdx.x >> 6];
-  const uint32_t i = trace_tile(blockIdx.x, gridDim.x) * kTraceBlock + threadIdx.x;
-  const unsigned long long t_start = job.wave_clock ? __builtin_amdgcn_s_memtime() : 0ull;
+  const uint32_t tile = job.order ? job.order[blockIdx.x] : trace_tile(blockIdx.x, gridDim.x);
+  const uint32_t i = tile * kTraceBlock + threadIdx.x;
+  const unsigned long long t_start = (job.wave_clock || job.cost) ? __builtin_amdgcn_s_memtime() : 0ull;
   const unsigned long long r_start = (job.wave_clock && job.wave_real) ? __builtin_amdgcn_s_memrealtime() : 0ull;
   const uint32_t n = job.n;
   TraceCtr ctr;
@@ -2268,6 +2331,7 @@ __global__ __launch_bounds__(kTraceBlock) BZR_TRACE_ATTR void k_trace(LensSet le
     job.status[i] = st;
     if (kMode == kModeStage && job.segments) job.segments[i] = seg;
   }
+  if (job.cost && threadIdx.x == 0u) job.cost[tile] = sched_bin(__builtin_amdgcn_s_memtime() - t_start);
   if (job.wave_clock && lane == 0u) {  // the wave's tile (ray index / 64): start tick and duration
     const unsigned long long t_end = __builtin_amdgcn_s_memtime();
     if (job.wave_real) {  // diagnostic: the wave's shader clock = d(s_memtime) / d(s_memrealtime) x 100 MHz
@@ -2646,6 +2710,22 @@ bzr_status run_fused(bzr_ctx *ctx, const LensSet &set, const TraceJob &job, uint
   TraceJob j = job;
   j.wave_clock = (ctx->wave_clock && ctx->wave_clock_cap >= (job.n + 63) / 64) ? ctx->wave_clock : nullptr;
   j.wave_real = ctx->wave_clock_real ? 1u : 0u;
+  j.order = nullptr;
+  j.cost = nullptr;
+  const uint32_t tiles = grid.x;
+  const bool sched = BZR_TRACE_SCHED && BZR_TRACE_RPL == 1 && tiles >= kSchedMinTiles;
+  if (sched) {  // this call's tile costs; the order of the last call of the same size, if any
+    if (ctx->sched_cap < tiles) {
+      if (ctx->sched) BZR_HIP(hipFree(ctx->sched));
+      ctx->sched = nullptr;
+      ctx->sched_cap = ctx->sched_waves = 0;
+      BZR_HIP(hipMalloc(&ctx->sched, ((size_t)2 * tiles + 2 * kSchedBins) * sizeof(uint32_t)));
+      BZR_HIP(hipMemsetAsync(ctx->sched + (size_t)2 * tiles, 0, kSchedBins * sizeof(uint32_t), ctx->stream));
+      ctx->sched_cap = tiles;
+    }
+    j.cost = ctx->sched;
+    if (ctx->sched_waves == tiles) j.order = ctx->sched + ctx->sched_cap;
+  }
 #if BZR_TRACE_RPL > 1
   constexpr uint32_t kRays = 64u * BZR_TRACE_RPL;  // rays per one-wave block (k_trace_r)
   const dim3 rgrid((job.n + kRays - 1) / kRays), rblock(64);
@@ -2670,6 +2750,15 @@ bzr_status run_fused(bzr_ctx *ctx, const LensSet &set, const TraceJob &job, uint
   }
 #endif
   BZR_HIP(hipGetLastError());
+  if (sched) {  // the next call's order: tiles longest-first (counting sort of the cost bins)
+    uint32_t *order = ctx->sched + ctx->sched_cap, *hist = ctx->sched + (size_t)2 * ctx->sched_cap, *offs = hist + kSchedBins;
+    const dim3 sg((tiles + kSchedThreads - 1) / kSchedThreads);
+    hipLaunchKernelGGL(k_sched_count, sg, dim3(kSchedThreads), 0, ctx->stream, ctx->sched, tiles, hist);
+    hipLaunchKernelGGL(k_sched_scan, dim3(1), dim3(kSchedBins), 0, ctx->stream, hist, offs);
+    hipLaunchKernelGGL(k_sched_place, sg, dim3(kSchedThreads), 0, ctx->stream, ctx->sched, tiles, offs, order);
+    BZR_HIP(hipGetLastError());
+    ctx->sched_waves = tiles;
+  }
   return BZR_OK;
 }
 
@@ -2797,6 +2886,7 @@ extern "C" bzr_status bzr_ctx_destroy(bzr_ctx *ctx) {
   if (ctx->work) (void)hipFree(ctx->work);
   if (ctx->counters) (void)hipFree(ctx->counters);
   if (ctx->pack) (void)hipFree(ctx->pack);
+  if (ctx->sched) (void)hipFree(ctx->sched);
   (void)hipStreamDestroy(ctx->own);
   delete ctx;
   return BZR_OK;
