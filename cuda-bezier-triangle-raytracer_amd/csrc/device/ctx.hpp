@@ -44,4 +44,5 @@ struct bzr_ctx {
   uint32_t *sched = nullptr;
   uint32_t sched_cap = 0;    // waves the buffer holds
   uint32_t sched_waves = 0;  // waves of the call whose order is ready (0: none)
+  uint32_t sched_calls = 0;  // calls since the order was first built for this size (rebuilt every BZR_TRACE_SCHED_REFRESH)
 };

@@ -2230,6 +2230,12 @@ __device__ __forceinline__ uint32_t trace_tile(uint32_t b, uint32_t nblocks) {
 #ifndef BZR_TRACE_SCHED
 #define BZR_TRACE_SCHED 1
 #endif
+// BZR_TRACE_SCHED_REFRESH (default 16): the order is rebuilt from the latest costs on the first call of a size
+// and then every this many calls (the three order kernels cost a short frame with others in flight ~8 % when
+// run on every call; the costs of a frame loop's tiles barely change from frame to frame).
+#ifndef BZR_TRACE_SCHED_REFRESH
+#define BZR_TRACE_SCHED_REFRESH 16
+#endif
 constexpr uint32_t kSchedBins = 128, kSchedMinTiles = 2048, kSchedThreads = 256;
 __device__ __forceinline__ uint32_t sched_bin(unsigned long long cycles) {
   const uint32_t c = static_cast<uint32_t>(cycles > 0xFFFFFFFFull ? 0xFFFFFFFFull : cycles) | 4u;
@@ -2724,8 +2730,14 @@ bzr_status run_fused(bzr_ctx *ctx, const LensSet &set, const TraceJob &job, uint
       ctx->sched_cap = tiles;
     }
     j.cost = ctx->sched;
-    if (ctx->sched_waves == tiles) j.order = ctx->sched + ctx->sched_cap;
+    if (ctx->sched_waves == tiles) {
+      j.order = ctx->sched + ctx->sched_cap;
+      ++ctx->sched_calls;
+    } else {
+      ctx->sched_calls = 0;
+    }
   }
+  const bool rebuild = sched && ctx->sched_calls % BZR_TRACE_SCHED_REFRESH == 0;
 #if BZR_TRACE_RPL > 1
   constexpr uint32_t kRays = 64u * BZR_TRACE_RPL;  // rays per one-wave block (k_trace_r)
   const dim3 rgrid((job.n + kRays - 1) / kRays), rblock(64);
@@ -2750,7 +2762,7 @@ bzr_status run_fused(bzr_ctx *ctx, const LensSet &set, const TraceJob &job, uint
   }
 #endif
   BZR_HIP(hipGetLastError());
-  if (sched) {  // the next call's order: tiles longest-first (counting sort of the cost bins)
+  if (rebuild) {  // the next calls' order: tiles longest-first (counting sort of the cost bins)
     uint32_t *order = ctx->sched + ctx->sched_cap, *hist = ctx->sched + (size_t)2 * ctx->sched_cap, *offs = hist + kSchedBins;
     const dim3 sg((tiles + kSchedThreads - 1) / kSchedThreads);
     hipLaunchKernelGGL(k_sched_count, sg, dim3(kSchedThreads), 0, ctx->stream, ctx->sched, tiles, hist);
