@@ -136,9 +136,19 @@ __device__ __forceinline__ uint32_t deal_blocks(uint32_t b, uint32_t nblocks) {
 // at once, as in k_trace; 256 (4 waves sharing a CU's scalar cache on neighbouring rays, rounds 1-3) measured
 // 0.5-1 % slower on cfg5 and 0.1-0.2 % on cfg3 at bench level, 128 4 % slower on cfg3
 // (profiles/r04_bench_ab_trav_block.jsonl).
-#ifndef BZR_TRAV_BLOCK
-#define BZR_TRAV_BLOCK 64
+// BZR_TRAV_ABLOCK (A/B knob, default 0): the always list's bundle pre-test once per block instead of once per
+// wave.  Before the walk every wave's bundle is in LDS; the block's union bundle tests up to kAblockMax
+// always-listed patches, one per thread, and keeps a mask in LDS.  1: each wave gate-tests the block-kept
+// patches per lane; 2: each wave first re-tests the block-kept patches against its own bundle in one round
+// (compacted), then gate-tests its survivors.  Implies 256-thread blocks.  Either way a dropped patch is one
+// no ray of the block (so of the wave) can pass: the candidates are unchanged.
+#ifndef BZR_TRAV_ABLOCK
+#define BZR_TRAV_ABLOCK 0
 #endif
+#ifndef BZR_TRAV_BLOCK
+#define BZR_TRAV_BLOCK (BZR_TRAV_ABLOCK ? 256 : 64)
+#endif
+constexpr uint32_t kAblockMax = 1024;  // always-listed patches the block pre-test covers (else per wave)
 constexpr int kTravBlock = BZR_TRAV_BLOCK;
 // BZR_SLAB_FMA (default 1): the traversal slab test as fma(lo, inv, -s*inv) (mirrored by bvh.cpp slab_h).
 #ifndef BZR_SLAB_FMA
@@ -581,6 +591,7 @@ __device__ __forceinline__ uint32_t t_order(float t) {
 
 // Number of lanes below this one in `mask`.
 __device__ __forceinline__ uint32_t popc64_(unsigned long long m) { return (uint32_t)__popcll(m); }
+__device__ __forceinline__ bool lane_bit64(unsigned long long m, uint32_t lane) { return ((m >> lane) & 1ull) != 0ull; }
 __device__ __forceinline__ uint32_t lanes_below(unsigned long long mask) {
   return __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(mask >> 32),
                                    __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(mask), 0u));
@@ -993,7 +1004,8 @@ __device__ __forceinline__ void list_candidate(bool pass, uint32_t b, const Work
 __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__restrict__ rays, uint32_t ld,
                                               uint32_t off, const uint32_t *__restrict__ alive, uint32_t n,
                                               const Work &w, unsigned long long *counters, uint32_t i, uint32_t *stk,
-                                              float *bl, uint32_t *pend, uint32_t *raw) {
+                                              float *bl, uint32_t *pend, uint32_t *raw, float *ubl = nullptr,
+                                              unsigned long long *akeep = nullptr) {
 #if BZR_TRAV_PHASES
   unsigned long long ph_acc[6] = {0ull, 0ull, 0ull, 0ull, 0ull, 0ull}, ph_t = __builtin_amdgcn_s_memtime();
   uint32_t ph_cur = 0;
@@ -1046,6 +1058,34 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
   uint32_t npend = 0, pi = 0;  // leaves queued in pend, next to gate-test (uniform)
 #if BZR_TRAV_PRETEST
   uint32_t nraw = 0;  // leaves queued in raw, not yet pre-tested
+#endif
+#if BZR_TRAV_ABLOCK
+  // the always list's block pre-test (every thread of the block gets here: no early exit above)
+  const bool ablock = m.n_always > 0u && m.n_always <= kAblockMax;
+  if (ablock) {
+    if (!walk) bundle_setup_dpp(active, s, d, bl, threadIdx.x & 63u);  // (an empty wave's bundle is the identity)
+    __syncthreads();
+    if (threadIdx.x < 13u) {  // the union over the block's waves with rays (bl - wave * kBundleWords: wave 0's)
+      const float *b0 = bl - (threadIdx.x >> 6) * kBundleWords;
+      const uint32_t k = threadIdx.x;
+      float v = k < 12u ? ((k % 6u) < 3u ? __builtin_inff() : -__builtin_inff()) : 1.0f;
+      bool any = false;
+      for (uint32_t q = 0; q < (uint32_t)kTravBlock / 64u; ++q) {
+        const float *bq = b0 + q * kBundleWords;
+        if (!(bq[0] <= bq[3])) continue;  // no active ray in wave q
+        any = true;
+        const float x = bq[k];
+        v = k == 12u ? fminf(v, x) : ((k % 6u) < 3u ? fminf(v, x) : fmaxf(v, x));
+      }
+      ubl[k] = (k == 12u && !any) ? 0.0f : v;
+    }
+    __syncthreads();
+    for (uint32_t base = 0; base < m.n_always; base += kTravBlock) {
+      const unsigned long long km = __ballot(always_bundle_keep(m.always, base + threadIdx.x, m.n_always, ubl));
+      if ((threadIdx.x & 63u) == 0u) akeep[(base + threadIdx.x) >> 6] = km;
+    }
+    __syncthreads();
+  }
 #endif
   while (bwalk) {
     if (pi < npend) {
@@ -1188,6 +1228,48 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
     if (!walk)  // (the bundle walk built it already)
 #endif
       bundle_to_lds(active, s, d, bl, threadIdx.x & 63u);
+#if BZR_TRAV_ABLOCK
+    if (ablock) {
+      const uint32_t lane = threadIdx.x & 63u, words = (m.n_always + 63u) / 64u;
+#if BZR_TRAV_ABLOCK == 2
+      // the block-kept patches compacted into the wave's (now idle) pend buffer, re-tested with its own bundle
+      uint32_t total = 0;
+      for (uint32_t q = 0; q < words; ++q) {
+        const unsigned long long kq = akeep[q];
+        if (lane_bit64(kq, lane)) pend[total + lanes_below(kq)] = q * 64u + lane;
+        total += (uint32_t)__popcll(kq);
+      }
+      __builtin_amdgcn_wave_barrier();
+      for (uint32_t r0 = 0; r0 < total; r0 += 64u) {
+        const uint32_t k = r0 + lane;
+        const uint32_t id = k < total ? pend[k] : 0u;
+        unsigned long long am = __ballot(k < total && always_bundle_keep(m.always, id, m.n_always, bl));
+        for (; am; am &= am - 1ull) {
+          uint32_t b;
+          if (counters) {
+            ++c_leaves;
+            c_gates += (uint32_t)__popcll(__ballot(active));
+          }
+          const uint32_t patch = __builtin_amdgcn_readfirstlane(pend[r0 + __builtin_ctzll(am)]);
+          const bool pass = always_gate(m.always, patch, active, s, d, b);
+          list_candidate(pass, b, w, n, i, cnt);
+        }
+      }
+#else
+      for (uint32_t q = 0; q < words; ++q) {
+        for (unsigned long long am = akeep[q]; am; am &= am - 1ull) {
+          uint32_t b;
+          if (counters) {
+            ++c_leaves;
+            c_gates += (uint32_t)__popcll(__ballot(active));
+          }
+          const bool pass = always_gate(m.always, q * 64u + __builtin_ctzll(am), active, s, d, b);
+          list_candidate(pass, b, w, n, i, cnt);
+        }
+      }
+#endif
+    } else
+#endif
     for (uint32_t ab = 0; ab * 64u < m.n_always; ++ab) {
       unsigned long long am = __ballot(always_bundle_keep(m.always, ab * 64u + (threadIdx.x & 63u), m.n_always, bl));
       for (; am; am &= am - 1ull) {
@@ -1314,8 +1396,16 @@ __global__ __launch_bounds__(kTravBlock) BZR_TRAV_ATTR void k_traverse(MeshView 
   uint32_t *wraw = nullptr;
 #endif
   const uint32_t b = deal_blocks<BZR_TRAV_XCD>(blockIdx.x, gridDim.x);
+#if BZR_TRAV_ABLOCK
+  static_assert(BZR_TRAV_BUNDLE, "BZR_TRAV_ABLOCK needs the bundle walk");
+  __shared__ float ubl[16];                                  // the block's union bundle (words 0..12)
+  __shared__ unsigned long long akeep[kAblockMax / 64u];     // block-kept always-listed patches
+  traverse_rays(m, rays, ld, off, alive, n, w, counters, b * kTravBlock + threadIdx.x, stack[threadIdx.x >> 6],
+                bundle[threadIdx.x >> 6], wpend, wraw, ubl, akeep);
+#else
   traverse_rays(m, rays, ld, off, alive, n, w, counters, b * kTravBlock + threadIdx.x, stack[threadIdx.x >> 6],
                 bundle[threadIdx.x >> 6], wpend, wraw);
+#endif
 }
 
 
