@@ -136,19 +136,21 @@ __device__ __forceinline__ uint32_t deal_blocks(uint32_t b, uint32_t nblocks) {
 // at once, as in k_trace; 256 (4 waves sharing a CU's scalar cache on neighbouring rays, rounds 1-3) measured
 // 0.5-1 % slower on cfg5 and 0.1-0.2 % on cfg3 at bench level, 128 4 % slower on cfg3
 // (profiles/r04_bench_ab_trav_block.jsonl).
-// BZR_TRAV_ABLOCK (A/B knob, default 0): the always list's bundle pre-test once per block instead of once per
-// wave.  Before the walk every wave's bundle is in LDS; the block's union bundle tests up to kAblockMax
-// always-listed patches, one per thread, and keeps a mask in LDS.  1: each wave gate-tests the block-kept
-// patches per lane; 2: each wave first re-tests the block-kept patches against its own bundle in one round
-// (compacted), then gate-tests its survivors.  Implies 256-thread blocks.  Either way a dropped patch is one
-// no ray of the block (so of the wave) can pass: the candidates are unchanged.
+// BZR_TRAV_ABLOCK: the always list's bundle pre-test once per 256-thread block instead of once per wave, for
+// meshes whose always list takes more than one 64-patch round (kAblockMin < n_always <= kAblockMax; others keep
+// the one-wave kernel).  Before the walk every wave's bundle is in LDS; the block's union bundle tests the
+// always-listed patches, one per thread, and keeps a mask in LDS.  1 (default): each wave gate-tests the
+// block-kept patches per lane; 2: each wave first re-tests the block-kept patches against its own bundle in
+// one (compacted) round; 0: off.  A dropped patch is one no ray of the block (so of the wave) can pass: the
+// candidates are unchanged.  cfg5 (131 always-listed patches): k_traverse 4.01 -> 3.84 ms per frame with 1,
+// 4.05 with 2 (profiles/r05_ab_traverse_ablock.jsonl).
 #ifndef BZR_TRAV_ABLOCK
-#define BZR_TRAV_ABLOCK 0
+#define BZR_TRAV_ABLOCK 1
 #endif
 #ifndef BZR_TRAV_BLOCK
-#define BZR_TRAV_BLOCK (BZR_TRAV_ABLOCK ? 256 : 64)
+#define BZR_TRAV_BLOCK 64
 #endif
-constexpr uint32_t kAblockMax = 1024;  // always-listed patches the block pre-test covers (else per wave)
+constexpr uint32_t kAblockMin = 64, kAblockMax = 1024, kAblockBlock = 256;
 constexpr int kTravBlock = BZR_TRAV_BLOCK;
 // BZR_SLAB_FMA (default 1): the traversal slab test as fma(lo, inv, -s*inv) (mirrored by bvh.cpp slab_h).
 #ifndef BZR_SLAB_FMA
@@ -1001,6 +1003,7 @@ __device__ __forceinline__ void list_candidate(bool pass, uint32_t b, const Work
 }
 // Candidate search.  `alive` (optional): a ray is traced iff alive[off + i] != BZR_RR_NONE.
 // One wave's 64 rays i (lane l of the wave holds ray i); `stk` is the wave's LDS stack.
+template <int kBlk, int kAblock>
 __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__restrict__ rays, uint32_t ld,
                                               uint32_t off, const uint32_t *__restrict__ alive, uint32_t n,
                                               const Work &w, unsigned long long *counters, uint32_t i, uint32_t *stk,
@@ -1059,10 +1062,8 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
 #if BZR_TRAV_PRETEST
   uint32_t nraw = 0;  // leaves queued in raw, not yet pre-tested
 #endif
-#if BZR_TRAV_ABLOCK
   // the always list's block pre-test (every thread of the block gets here: no early exit above)
-  const bool ablock = m.n_always > 0u && m.n_always <= kAblockMax;
-  if (ablock) {
+  if constexpr (kAblock != 0) {
     if (!walk) bundle_setup_dpp(active, s, d, bl, threadIdx.x & 63u);  // (an empty wave's bundle is the identity)
     __syncthreads();
     if (threadIdx.x < 13u) {  // the union over the block's waves with rays (bl - wave * kBundleWords: wave 0's)
@@ -1070,7 +1071,7 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
       const uint32_t k = threadIdx.x;
       float v = k < 12u ? ((k % 6u) < 3u ? __builtin_inff() : -__builtin_inff()) : 1.0f;
       bool any = false;
-      for (uint32_t q = 0; q < (uint32_t)kTravBlock / 64u; ++q) {
+      for (uint32_t q = 0; q < (uint32_t)kBlk / 64u; ++q) {
         const float *bq = b0 + q * kBundleWords;
         if (!(bq[0] <= bq[3])) continue;  // no active ray in wave q
         any = true;
@@ -1080,13 +1081,12 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
       ubl[k] = (k == 12u && !any) ? 0.0f : v;
     }
     __syncthreads();
-    for (uint32_t base = 0; base < m.n_always; base += kTravBlock) {
+    for (uint32_t base = 0; base < m.n_always; base += kBlk) {
       const unsigned long long km = __ballot(always_bundle_keep(m.always, base + threadIdx.x, m.n_always, ubl));
       if ((threadIdx.x & 63u) == 0u) akeep[(base + threadIdx.x) >> 6] = km;
     }
     __syncthreads();
   }
-#endif
   while (bwalk) {
     if (pi < npend) {
       BZR_PHASE(1)
@@ -1228,10 +1228,9 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
     if (!walk)  // (the bundle walk built it already)
 #endif
       bundle_to_lds(active, s, d, bl, threadIdx.x & 63u);
-#if BZR_TRAV_ABLOCK
-    if (ablock) {
+    if constexpr (kAblock != 0) {
       const uint32_t lane = threadIdx.x & 63u, words = (m.n_always + 63u) / 64u;
-#if BZR_TRAV_ABLOCK == 2
+      if constexpr (kAblock == 2) {
       // the block-kept patches compacted into the wave's (now idle) pend buffer, re-tested with its own bundle
       uint32_t total = 0;
       for (uint32_t q = 0; q < words; ++q) {
@@ -1255,7 +1254,7 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
           list_candidate(pass, b, w, n, i, cnt);
         }
       }
-#else
+      } else {
       for (uint32_t q = 0; q < words; ++q) {
         for (unsigned long long am = akeep[q]; am; am &= am - 1ull) {
           uint32_t b;
@@ -1267,9 +1266,8 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
           list_candidate(pass, b, w, n, i, cnt);
         }
       }
-#endif
+      }
     } else
-#endif
     for (uint32_t ab = 0; ab * 64u < m.n_always; ++ab) {
       unsigned long long am = __ballot(always_bundle_keep(m.always, ab * 64u + (threadIdx.x & 63u), m.n_always, bl));
       for (; am; am &= am - 1ull) {
@@ -1378,34 +1376,35 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
 #else
 #define BZR_TRAV_ATTR
 #endif
-__global__ __launch_bounds__(kTravBlock) BZR_TRAV_ATTR void k_traverse(MeshView m, const float *__restrict__ rays, uint32_t ld,
+template <int kBlk, int kAblock>
+__global__ __launch_bounds__(kBlk) BZR_TRAV_ATTR void k_traverse(MeshView m, const float *__restrict__ rays, uint32_t ld,
                                                          uint32_t off, const uint32_t *__restrict__ alive, uint32_t n,
                                                          Work w, unsigned long long *counters) {
-  __shared__ uint32_t stack[kTravBlock / 64][kTravStack];
-  __shared__ float bundle[kTravBlock / 64][kBundleWords];  // the wave's ray bundle (bundle walk, always list)
+  __shared__ uint32_t stack[kBlk / 64][kTravStack];
+  __shared__ float bundle[kBlk / 64][kBundleWords];  // the wave's ray bundle (bundle walk, always list)
 #if BZR_TRAV_BUNDLE
-  __shared__ uint32_t pend[kTravBlock / 64][BZR_TRAV_PRETEST ? 128 : 64];  // the bundle walk's queued leaf slots
+  __shared__ uint32_t pend[kBlk / 64][BZR_TRAV_PRETEST ? 128 : 64];  // the bundle walk's queued leaf slots
   uint32_t *wpend = pend[threadIdx.x >> 6];
 #else
   uint32_t *wpend = nullptr;
 #endif
 #if BZR_TRAV_BUNDLE && BZR_TRAV_PRETEST
-  __shared__ uint32_t raw[kTravBlock / 64][128];  // leaves before the pre-test (up to two batches' worth)
+  __shared__ uint32_t raw[kBlk / 64][128];  // leaves before the pre-test (up to two batches' worth)
   uint32_t *wraw = raw[threadIdx.x >> 6];
 #else
   uint32_t *wraw = nullptr;
 #endif
   const uint32_t b = deal_blocks<BZR_TRAV_XCD>(blockIdx.x, gridDim.x);
-#if BZR_TRAV_ABLOCK
-  static_assert(BZR_TRAV_BUNDLE, "BZR_TRAV_ABLOCK needs the bundle walk");
-  __shared__ float ubl[16];                                  // the block's union bundle (words 0..12)
-  __shared__ unsigned long long akeep[kAblockMax / 64u];     // block-kept always-listed patches
-  traverse_rays(m, rays, ld, off, alive, n, w, counters, b * kTravBlock + threadIdx.x, stack[threadIdx.x >> 6],
-                bundle[threadIdx.x >> 6], wpend, wraw, ubl, akeep);
-#else
-  traverse_rays(m, rays, ld, off, alive, n, w, counters, b * kTravBlock + threadIdx.x, stack[threadIdx.x >> 6],
-                bundle[threadIdx.x >> 6], wpend, wraw);
-#endif
+  if constexpr (kAblock != 0) {
+    static_assert(!kAblock || BZR_TRAV_BUNDLE, "BZR_TRAV_ABLOCK needs the bundle walk");
+    __shared__ float ubl[16];                                  // the block's union bundle (words 0..12)
+    __shared__ unsigned long long akeep[kAblockMax / 64u];     // block-kept always-listed patches
+    traverse_rays<kBlk, kAblock>(m, rays, ld, off, alive, n, w, counters, b * kBlk + threadIdx.x, stack[threadIdx.x >> 6],
+                                 bundle[threadIdx.x >> 6], wpend, wraw, ubl, akeep);
+  } else {
+    traverse_rays<kBlk, 0>(m, rays, ld, off, alive, n, w, counters, b * kBlk + threadIdx.x, stack[threadIdx.x >> 6],
+                           bundle[threadIdx.x >> 6], wpend, wraw);
+  }
 }
 
 
@@ -2763,8 +2762,13 @@ bzr_status run_culled(bzr_ctx *ctx, const MeshView &mv, const float *rays, uint3
     BZR_HIP(hipMemsetAsync(w.ctr, 0, reinterpret_cast<char *>(w.hist + hn + 1) - reinterpret_cast<char *>(w.ctr),
                            ctx->stream));
   ctx->zero_ctr = nullptr;  // valid again only once this segment is fully enqueued
-  launch_on(ctx, ctx->stream, dim3(kTravBlock), BZR_KERNEL_TRAVERSE, k_traverse, dim3((n + kTravBlock - 1) / kTravBlock),
-            mv, rays, ld, off, alive, n, w, (ctx->counting && ctx->counters) ? ctx->counters : nullptr);
+  unsigned long long *const ctr = (ctx->counting && ctx->counters) ? ctx->counters : nullptr;
+  if (BZR_TRAV_ABLOCK && mv.n_always > kAblockMin && mv.n_always <= kAblockMax)  // block-level always-list pre-test
+    launch_on(ctx, ctx->stream, dim3(kAblockBlock), BZR_KERNEL_TRAVERSE, k_traverse<kAblockBlock, BZR_TRAV_ABLOCK>,
+              dim3((n + kAblockBlock - 1) / kAblockBlock), mv, rays, ld, off, alive, n, w, ctr);
+  else
+    launch_on(ctx, ctx->stream, dim3(kTravBlock), BZR_KERNEL_TRAVERSE, k_traverse<kTravBlock, 0>,
+              dim3((n + kTravBlock - 1) / kTravBlock), mv, rays, ld, off, alive, n, w, ctr);
   {
     Span sp(ctx, BZR_KERNEL_BUCKET);
     if (small_scan)
