@@ -996,9 +996,52 @@ __device__ __forceinline__ bool bundle_gate_keep(const float *B, float4 q0, floa
 // b is wave-uniform, so one atomic without return per wave -- and ranking the pairs in k_place instead of
 // after the walk: k_traverse -1.6 % on cfg5 and -9 % on cfg3, but k_place's grouped ranking atomics cost more
 // than that, cfg3 frames +7.6 %; profiles/r04_ab_rank_late.jsonl.)
+// BZR_RANK_EARLY (default 1): each listed group (the lanes whose gate of the wave-uniform patch b passed) takes
+// its ranks in b's bucket right away -- one returning atomic by its first lane -- and stores them at the next
+// listing, by when the atomic has long returned (one group pending: its base in the first lane's VGPR).  This
+// replaces the ranking pass after the walk (the candidates' reload, a ballot loop per list slot grouping the
+// lanes by patch, and the atomics' round trip at the end of the wave: 13 % of a cfg5 wave, 22 % of a cfg3
+// one).  A ray that later overflows its list keeps its ranked places; k_place fills them with idle (kNoPair)
+// records.
+#ifndef BZR_RANK_EARLY
+#define BZR_RANK_EARLY 1
+#endif
+struct RankPend {  // the last listed group of the wave (BZR_RANK_EARLY)
+  uint32_t base = 0u;           // its first place in the bucket (valid in its first lane)
+  unsigned long long g = 0ull;  // its lanes
+};
+// Store the pending group's ranks: a lane's slot is its list count - 1 (its count changes only at a listing,
+// after this; the overflow flag keeps the low bits).
+__device__ __forceinline__ void rank_flush(RankPend &pr, const Work &w, uint32_t n, uint32_t i, uint32_t cnt) {
+  if (pr.g) {
+    const uint32_t bs = __builtin_amdgcn_readlane(pr.base, (uint32_t)__builtin_ctzll(pr.g));
+    if (lane_bit64(pr.g, threadIdx.x & 63u))
+      w.rank[(size_t)((cnt & (kOverflow - 1u)) - 1u) * n + i] = bs + lanes_below(pr.g);
+    pr.g = 0ull;
+  }
+}
 __device__ __forceinline__ void list_candidate(bool pass, uint32_t b, const Work &w, uint32_t n, uint32_t i,
-                                               uint32_t &cnt) {
-  if (pass && cnt < kMaxCand) w.cand[(size_t)cnt * n + i] = b;
+                                               uint32_t &cnt, RankPend &pr) {
+  const bool lst = pass && cnt < kMaxCand;
+#if BZR_RANK_EARLY == 1
+  rank_flush(pr, w, n, i, cnt);
+#endif
+#if BZR_RANK_EARLY
+  const unsigned long long g = __ballot(lst);
+  if (g) {
+    const uint32_t leader = (uint32_t)__builtin_ctzll(g);
+    uint32_t base = 0u;
+    if ((threadIdx.x & 63u) == leader) base = atomicAdd(&w.hist[b], (uint32_t)__popcll(g));
+#if BZR_RANK_EARLY == 1
+    pr.base = base;
+    pr.g = g;
+#else  // 2: wait for the atomic right here (no state across the walk)
+    const uint32_t bs = __builtin_amdgcn_readlane(base, leader);
+    if (lst) w.rank[(size_t)cnt * n + i] = bs + lanes_below(g);
+#endif
+  }
+#endif
+  if (lst) w.cand[(size_t)cnt * n + i] = b;
   if (pass) cnt = cnt < kMaxCand ? cnt + 1 : (cnt | kOverflow);
 }
 // Candidate search.  `alive` (optional): a ray is traced iff alive[off + i] != BZR_RR_NONE.
@@ -1024,6 +1067,7 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
   }
 #endif
   uint32_t cnt = 0;
+  RankPend rpend;  // BZR_RANK_EARLY: the last listed group's ranks, stored at the next listing
   // gate-region boxes hold for ray origins within s_max (bvh.cpp); farther rays take the full scan
   if (active && !(fmaxf(fmaxf(fabsf(s.x), fabsf(s.y)), fabsf(s.z)) <= m.s_max)) {
     cnt |= kOverflow;
@@ -1035,8 +1079,6 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
   const bzr_host::Bvh4Node *nodes = near_tier ? m.nodes_near : m.nodes;
   const bzr_host::Bvh4ObbNode *obb = near_tier ? m.obb_near : m.obb;
   const float4 *leaf = near_tier ? m.leaf_near : m.leaf;
-  const f3 inv = mk(safe_inv(d.x), safe_inv(d.y), safe_inv(d.z));
-  const f3 sinv = mk(s.x * inv.x, s.y * inv.y, s.z * inv.z);
   int sp = 0;  // the node to visit next stays in a scalar register; the other hit children go to stk
   uint32_t next = (m.n > 0 && __any(active)) ? 0u : 0xFFFFFFFFu;
   unsigned long long next_hm = 0ull;
@@ -1105,10 +1147,10 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
         c_gates += (two ? 2u : 1u) * (uint32_t)__popcll(__ballot(active));
       }
       list_candidate(active & planar_gate(leaf_q(r0, 0), leaf_q(r0, 1), leaf_q(r0, 2), leaf_q(r0, 3), s, d), r0[15], w,
-                     n, i, cnt);
+                     n, i, cnt, rpend);
       if (two)
         list_candidate(active & planar_gate(leaf_q(r1, 0), leaf_q(r1, 1), leaf_q(r1, 2), leaf_q(r1, 3), s, d), r1[15],
-                       w, n, i, cnt);
+                       w, n, i, cnt, rpend);
 #else
       const uint32_t slot = __builtin_amdgcn_readfirstlane(pend[pi]);
       ++pi;
@@ -1118,7 +1160,7 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
         c_gates += (uint32_t)__popcll(__ballot(active));
       }
       list_candidate(active & planar_gate(leaf_q(r, 0), leaf_q(r, 1), leaf_q(r, 2), leaf_q(r, 3), s, d), r[15], w, n,
-                     i, cnt);
+                     i, cnt, rpend);
 #endif
       continue;
     }
@@ -1189,6 +1231,9 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
   }
 #endif
   BZR_PHASE(3)
+#if !BZR_TRAV_BUNDLE  // (the bundle walk ends with an empty stack and tests wide waves' nodes per lane itself)
+  const f3 inv = mk(safe_inv(d.x), safe_inv(d.y), safe_inv(d.z));
+  const f3 sinv = mk(s.x * inv.x, s.y * inv.y, s.z * inv.z);
   while (next != 0xFFFFFFFFu || sp > 0) {  // the per-lane walk
     const uint32_t node = next != 0xFFFFFFFFu ? next : __builtin_amdgcn_readfirstlane(stk[--sp]);
     next = 0xFFFFFFFFu;
@@ -1210,7 +1255,7 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
           ++c_leaves;
           c_gates += (uint32_t)__popcll(hm);
         }
-        list_candidate(hit[c] & planar_gate(q0, q1, q2, q3, s, d), r[15], w, n, i, cnt);
+        list_candidate(hit[c] & planar_gate(q0, q1, q2, q3, s, d), r[15], w, n, i, cnt, rpend);
       } else {
         if (next != 0xFFFFFFFFu) {
           if (sp < kTravStack) stk[sp++] = next;
@@ -1221,6 +1266,7 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
       }
     }
   }
+#endif
   // the always list (patches without a proven gate region, bvh.cpp): gate-tested for every active ray
   BZR_PHASE(4)
   if (m.n_always && __any(active)) {
@@ -1251,7 +1297,7 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
           }
           const uint32_t patch = __builtin_amdgcn_readfirstlane(pend[r0 + __builtin_ctzll(am)]);
           const bool pass = always_gate(m.always, patch, active, s, d, b);
-          list_candidate(pass, b, w, n, i, cnt);
+          list_candidate(pass, b, w, n, i, cnt, rpend);
         }
       }
       } else {
@@ -1263,7 +1309,7 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
             c_gates += (uint32_t)__popcll(__ballot(active));
           }
           const bool pass = always_gate(m.always, q * 64u + __builtin_ctzll(am), active, s, d, b);
-          list_candidate(pass, b, w, n, i, cnt);
+          list_candidate(pass, b, w, n, i, cnt, rpend);
         }
       }
       }
@@ -1277,7 +1323,7 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
           c_gates += (uint32_t)__popcll(__ballot(active));
         }
         const bool pass = always_gate(m.always, ab * 64u + __builtin_ctzll(am), active, s, d, b);
-        list_candidate(pass, b, w, n, i, cnt);
+        list_candidate(pass, b, w, n, i, cnt, rpend);
       }
     }
 
@@ -1291,10 +1337,14 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
     const uint32_t which = lane == 0u ? BZR_COUNTER_NODE_VISITS : (lane == 1u ? BZR_COUNTER_LEAF_FETCHES : BZR_COUNTER_GATE_TESTS);
     if (!BZR_TRAV_PHASES && lane < 3u && v) atomicAdd(&counters[(size_t)rep * BZR_COUNTER_COUNT + which], (unsigned long long)v);
   }
+#if BZR_RANK_EARLY == 1
+  rank_flush(rpend, w, n, i, cnt);
+#endif
   if (i >= n) return;
   w.count[i] = cnt;
   w.key[i] = ~0ull;
   if (cnt > kMaxCand) w.ovf[atomicAdd(&w.ctr[1], 1u)] = i;
+#if !BZR_RANK_EARLY
   // Rank of each (ray, patch) pair within its patch bucket.  Neighbouring rays mostly share
   // patches: the lanes naming the same patch form a group (found with ballots, no memory traffic),
   // each group's first lane adds the group size -- all groups in one atomic instruction -- and the
@@ -1339,6 +1389,10 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
       if (j0 + k < listed) w.rank[(size_t)(j0 + k) * n + i] = bs + below[k];
     }
   }
+#else
+  const uint32_t lane = threadIdx.x & 63u;
+  (void)lane;
+#endif
 #if BZR_TRAV_PHASES
   BZR_PHASE(0)
   if (counters && lane < 6u) {
@@ -1443,8 +1497,19 @@ __global__ __launch_bounds__(kBlock) void k_place(uint32_t n, uint32_t nb, Work 
     if ((threadIdx.x & 63u) == 0u && sum) atomicAdd(pair_count, sum);
   }
   if (t >= n) return;
-  const uint32_t cnt = w.count[t];
-  if (cnt > kMaxCand || cnt == 0) return;  // (an overflow ray's list is not ranked: the full scan takes it)
+  const uint32_t c0 = w.count[t];
+#if BZR_RANK_EARLY
+  // an overflow ray (the full scan takes it) had its listed pairs ranked in k_traverse: their places get idle
+  // kNoPair records (its patch in .y, as the dense chunks' padding), and the pair counter drops them
+  const bool idle = c0 > kMaxCand;
+  const uint32_t cnt = c0 & (kOverflow - 1u);
+  if (idle && cnt && pair_count) atomicSub(pair_count, cnt);
+#else
+  if (c0 > kMaxCand) return;  // (an overflow ray's list is not ranked: the full scan takes it)
+  const bool idle = false;
+  const uint32_t cnt = c0;
+#endif
+  if (cnt == 0) return;
   const unsigned long long tot = w.offs[nb];
   const uint32_t sparse0 = static_cast<uint32_t>(tot >> 32) * 64u;  // the sparse region's first pair
   // four list slots per round: their loads first, then the offsets, then the stores
@@ -1467,7 +1532,7 @@ __global__ __launch_bounds__(kBlock) void k_place(uint32_t n, uint32_t nb, Work 
       if (j0 + k >= cnt) break;
       const uint32_t dbase = static_cast<uint32_t>(o0[k] >> 32), dlen = 64u * (static_cast<uint32_t>(o1[k] >> 32) - dbase);
       const uint32_t p = r[k] < dlen ? dbase * 64u + r[k] : sparse0 + static_cast<uint32_t>(o0[k]) + (r[k] - dlen);
-      w.pairs[p] = make_uint2(t | ((j0 + k) << 26), b[k]);
+      w.pairs[p] = make_uint2(idle ? kNoPair : t | ((j0 + k) << 26), b[k]);
     }
   }
 }
