@@ -996,15 +996,17 @@ __device__ __forceinline__ bool bundle_gate_keep(const float *B, float4 q0, floa
 // b is wave-uniform, so one atomic without return per wave -- and ranking the pairs in k_place instead of
 // after the walk: k_traverse -1.6 % on cfg5 and -9 % on cfg3, but k_place's grouped ranking atomics cost more
 // than that, cfg3 frames +7.6 %; profiles/r04_ab_rank_late.jsonl.)
-// BZR_RANK_EARLY (default 1): each listed group (the lanes whose gate of the wave-uniform patch b passed) takes
-// its ranks in b's bucket right away -- one returning atomic by its first lane -- and stores them at the next
-// listing, by when the atomic has long returned (one group pending: its base in the first lane's VGPR).  This
-// replaces the ranking pass after the walk (the candidates' reload, a ballot loop per list slot grouping the
-// lanes by patch, and the atomics' round trip at the end of the wave: 13 % of a cfg5 wave, 22 % of a cfg3
-// one).  A ray that later overflows its list keeps its ranked places; k_place fills them with idle (kNoPair)
-// records.
+// BZR_RANK_EARLY (A/B knob, default 0): each listed group (the lanes whose gate of the wave-uniform patch b
+// passed) takes its ranks in b's bucket right away -- one returning atomic by its first lane -- instead of the
+// ranking pass after the walk (the candidates' reload, a ballot loop per list slot grouping the lanes by patch,
+// the atomics' round trip at the end of the wave: 13 % of a cfg5 wave, 22 % of a cfg3 one).  1: the ranks are
+// stored at the next listing (one group pending, its base in a VGPR across the walk); 2: stored at once (the
+// wave waits for each atomic).  A ray that later overflows its list keeps its ranked places; k_place fills them
+// with idle (kNoPair) records.  Both lose: cfg5 k_traverse 3.88 -> 4.45 (1) / 4.20 (2) ms per frame, cfg3 0.173
+// -> 0.201 / 0.187 (profiles/r05_ab_rank_early.jsonl): one atomic round trip per listing instead of one per four
+// list slots, and with 1 the pending base spills VGPRs at the 8-wave budget.
 #ifndef BZR_RANK_EARLY
-#define BZR_RANK_EARLY 1
+#define BZR_RANK_EARLY 0
 #endif
 struct RankPend {  // the last listed group of the wave (BZR_RANK_EARLY)
   uint32_t base = 0u;           // its first place in the bucket (valid in its first lane)
