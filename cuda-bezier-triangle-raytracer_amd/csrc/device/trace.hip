@@ -1008,9 +1008,12 @@ __device__ __forceinline__ bool bundle_gate_keep(const float *B, float4 q0, floa
 #ifndef BZR_RANK_EARLY
 #define BZR_RANK_EARLY 0
 #endif
-struct RankPend {  // the last listed group of the wave (BZR_RANK_EARLY)
+constexpr uint32_t kRankEntries = 64;  // BZR_RANK_EARLY 3: listings recorded per wave
+struct RankPend {  // the last listed group of the wave (BZR_RANK_EARLY 1); the wave's listings (3)
   uint32_t base = 0u;           // its first place in the bucket (valid in its first lane)
   unsigned long long g = 0ull;  // its lanes
+  uint32_t *ent = nullptr;      // 3: LDS [kRankEntries] patch, then [kRankEntries] lane masks (two words each)
+  uint32_t ne = 0u;             // 3: listings so far (uniform; past kRankEntries the wave ranks the old way)
 };
 // Store the pending group's ranks: a lane's slot is its list count - 1 (its count changes only at a listing,
 // after this; the overflow flag keeps the low bits).
@@ -1028,7 +1031,16 @@ __device__ __forceinline__ void list_candidate(bool pass, uint32_t b, const Work
 #if BZR_RANK_EARLY == 1
   rank_flush(pr, w, n, i, cnt);
 #endif
-#if BZR_RANK_EARLY
+#if BZR_RANK_EARLY == 3
+  const unsigned long long g = __ballot(lst);
+  if (g) {  // record the listing (patch, lanes) in the wave's LDS; ranked after the walk
+    if (pr.ne < kRankEntries && (threadIdx.x & 63u) == 0u) {
+      pr.ent[pr.ne] = b;
+      reinterpret_cast<unsigned long long *>(pr.ent + kRankEntries)[pr.ne] = g;
+    }
+    ++pr.ne;
+  }
+#elif BZR_RANK_EARLY
   const unsigned long long g = __ballot(lst);
   if (g) {
     const uint32_t leader = (uint32_t)__builtin_ctzll(g);
@@ -1037,6 +1049,8 @@ __device__ __forceinline__ void list_candidate(bool pass, uint32_t b, const Work
 #if BZR_RANK_EARLY == 1
     pr.base = base;
     pr.g = g;
+#elif BZR_RANK_EARLY == 3
+    (void)base;
 #else  // 2: wait for the atomic right here (no state across the walk)
     const uint32_t bs = __builtin_amdgcn_readlane(base, leader);
     if (lst) w.rank[(size_t)cnt * n + i] = bs + lanes_below(g);
@@ -1053,7 +1067,7 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
                                               uint32_t off, const uint32_t *__restrict__ alive, uint32_t n,
                                               const Work &w, unsigned long long *counters, uint32_t i, uint32_t *stk,
                                               float *bl, uint32_t *pend, uint32_t *raw, float *ubl = nullptr,
-                                              unsigned long long *akeep = nullptr) {
+                                              unsigned long long *akeep = nullptr, uint32_t *rk = nullptr) {
 #if BZR_TRAV_PHASES
   unsigned long long ph_acc[6] = {0ull, 0ull, 0ull, 0ull, 0ull, 0ull}, ph_t = __builtin_amdgcn_s_memtime();
   uint32_t ph_cur = 0;
@@ -1069,7 +1083,8 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
   }
 #endif
   uint32_t cnt = 0;
-  RankPend rpend;  // BZR_RANK_EARLY: the last listed group's ranks, stored at the next listing
+  RankPend rpend;  // BZR_RANK_EARLY: the last listed group's ranks, stored at the next listing (1); listings (3)
+  rpend.ent = rk;
   // gate-region boxes hold for ray origins within s_max (bvh.cpp); farther rays take the full scan
   if (active && !(fmaxf(fmaxf(fabsf(s.x), fabsf(s.y)), fabsf(s.z)) <= m.s_max)) {
     cnt |= kOverflow;
@@ -1346,7 +1361,33 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
   w.count[i] = cnt;
   w.key[i] = ~0ull;
   if (cnt > kMaxCand) w.ovf[atomicAdd(&w.ctr[1], 1u)] = i;
-#if !BZR_RANK_EARLY
+#if BZR_RANK_EARLY == 3
+  const uint32_t lane = threadIdx.x & 63u;
+  BZR_PHASE(5)
+  if (rpend.ne <= kRankEntries) {
+    // every recorded listing's atomic at once (lane e: listing e, its lanes minus the overflow rays, which rank
+    // nothing: the full scan takes them), one wait, then each listing's lanes store base + their rank in it --
+    // a lane's j-th listing is its list slot j
+    const unsigned long long ovf = __ballot(cnt > kMaxCand);
+    const uint32_t ne = rpend.ne;
+    const unsigned long long *eg = reinterpret_cast<const unsigned long long *>(rk + kRankEntries);
+    uint32_t base = 0u;
+    if (lane < ne) {
+      const unsigned long long g = eg[lane] & ~ovf;
+      if (g) base = atomicAdd(&w.hist[rk[lane]], (uint32_t)__popcll(g));
+    }
+    uint32_t slot = 0u;
+    for (uint32_t e = 0; e < ne; ++e) {
+      const unsigned long long g0 = eg[e];
+      const unsigned long long g = ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(g0 >> 32)) << 32) |
+                                   (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)g0);
+      const uint32_t bs = __builtin_amdgcn_readlane(base, e);
+      if (lane_bit64(g & ~ovf, lane)) w.rank[(size_t)slot * n + i] = bs + lanes_below(g & ~ovf);
+      slot += lane_bit64(g, lane) ? 1u : 0u;
+    }
+  } else {
+#endif
+#if !BZR_RANK_EARLY || BZR_RANK_EARLY == 3
   // Rank of each (ray, patch) pair within its patch bucket.  Neighbouring rays mostly share
   // patches: the lanes naming the same patch form a group (found with ballots, no memory traffic),
   // each group's first lane adds the group size -- all groups in one atomic instruction -- and the
@@ -1394,6 +1435,9 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
 #else
   const uint32_t lane = threadIdx.x & 63u;
   (void)lane;
+#endif
+#if BZR_RANK_EARLY == 3
+  }
 #endif
 #if BZR_TRAV_PHASES
   BZR_PHASE(0)
@@ -1451,15 +1495,21 @@ __global__ __launch_bounds__(kBlk) BZR_TRAV_ATTR void k_traverse(MeshView m, con
   uint32_t *wraw = nullptr;
 #endif
   const uint32_t b = deal_blocks<BZR_TRAV_XCD>(blockIdx.x, gridDim.x);
+#if BZR_RANK_EARLY == 3
+  __shared__ uint32_t rk[kBlk / 64][3 * kRankEntries];  // the wave's listings (patch, lane mask)
+  uint32_t *wrk = rk[threadIdx.x >> 6];
+#else
+  uint32_t *wrk = nullptr;
+#endif
   if constexpr (kAblock != 0) {
     static_assert(!kAblock || BZR_TRAV_BUNDLE, "BZR_TRAV_ABLOCK needs the bundle walk");
     __shared__ float ubl[16];                                  // the block's union bundle (words 0..12)
     __shared__ unsigned long long akeep[kAblockMax / 64u];     // block-kept always-listed patches
     traverse_rays<kBlk, kAblock>(m, rays, ld, off, alive, n, w, counters, b * kBlk + threadIdx.x, stack[threadIdx.x >> 6],
-                                 bundle[threadIdx.x >> 6], wpend, wraw, ubl, akeep);
+                                 bundle[threadIdx.x >> 6], wpend, wraw, ubl, akeep, wrk);
   } else {
     traverse_rays<kBlk, 0>(m, rays, ld, off, alive, n, w, counters, b * kBlk + threadIdx.x, stack[threadIdx.x >> 6],
-                           bundle[threadIdx.x >> 6], wpend, wraw);
+                           bundle[threadIdx.x >> 6], wpend, wraw, nullptr, nullptr, wrk);
   }
 }
 
