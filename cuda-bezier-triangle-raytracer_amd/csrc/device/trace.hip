@@ -1496,7 +1496,7 @@ __global__ __launch_bounds__(kBlk) BZR_TRAV_ATTR void k_traverse(MeshView m, con
 #endif
   const uint32_t b = deal_blocks<BZR_TRAV_XCD>(blockIdx.x, gridDim.x);
 #if BZR_RANK_EARLY == 3
-  __shared__ uint32_t rk[kBlk / 64][3 * kRankEntries];  // the wave's listings (patch, lane mask)
+  __shared__ __attribute__((aligned(8))) uint32_t rk[kBlk / 64][3 * kRankEntries];  // the wave's listings (patch, lane mask)
   uint32_t *wrk = rk[threadIdx.x >> 6];
 #else
   uint32_t *wrk = nullptr;
