@@ -1550,7 +1550,7 @@ __global__ __launch_bounds__(kBlock) void k_place(uint32_t n, uint32_t nb, Work 
   }
   if (t >= n) return;
   const uint32_t c0 = w.count[t];
-#if BZR_RANK_EARLY
+#if BZR_RANK_EARLY == 1 || BZR_RANK_EARLY == 2
   // an overflow ray (the full scan takes it) had its listed pairs ranked in k_traverse: their places get idle
   // kNoPair records (its patch in .y, as the dense chunks' padding), and the pair counter drops them
   const bool idle = c0 > kMaxCand;
