@@ -86,9 +86,10 @@ enum {
    * or more, which the staged encoding cannot hold), else staged.  The 256 is tuned for callers that keep
    * two or three frames in flight (bench.py, bzr_tiled with several slots): there the fused path wins from
    * ~256 rays per patch up.  A caller that traces ONE frame at a time and waits for it sees the fused
-   * frame's tail (its slowest waves, ~0.3-0.5 ms) undiluted; for such callers the staged path wins up to
-   * ~2000 rays per patch (cfg2, 341 rays per patch: staged 3 859 vs fused 2 916 Mrays/s on lone frames),
-   * so pass BZR_PIPELINE_STAGED explicitly there (DESIGN.md (a) "Which one runs"). */
+   * frame's tail (its slowest waves) undiluted; the fused path dispatches a context's repeated same-size
+   * calls longest-tile-first from the previous calls' costs, which shortens that tail (cfg2 lone frames
+   * 0.62 -> 0.40 ms), and lone cfg2 frames now run as fast fused as staged (0.395 vs 0.392 ms, 341 rays per
+   * patch).  The first call of a size, or calls of changing sizes, run in input order. */
   BZR_PIPELINE_STAGED = 8u,
   BZR_PIPELINE_FUSED = 16u
 };
