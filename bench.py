@@ -267,7 +267,7 @@ def verify_frame(a, cfg, chain, world, rank, side, height, ctx, meshes, ris, mod
     total = side * height
     host_bytes = total * (32 if chain else 52) * 3  # reference image + assembled image + temporaries
     if rank == 0:
-        if host_bytes > 24e9:
+        if host_bytes > 6e9:
             msg = f"skipped: {total} pixels ({host_bytes / 1e9:.0f} GB of host arrays)"
             out["frame"] = {"skipped": msg}
             if gather:
