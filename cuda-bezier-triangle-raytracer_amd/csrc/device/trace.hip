@@ -1096,6 +1096,11 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
   const bzr_host::Bvh4Node *nodes = near_tier ? m.nodes_near : m.nodes;
   const bzr_host::Bvh4ObbNode *obb = near_tier ? m.obb_near : m.obb;
   const float4 *leaf = near_tier ? m.leaf_near : m.leaf;
+  // (the per-lane walk's reciprocals: that walk never runs after the bundle walk, which ends with an empty
+  // stack, but dropping them here put k_traverse<256, 1> at 3 VGPR spills (scratch) instead of 0 -- the
+  // register allocator is sensitive to it; kept)
+  const f3 inv = mk(safe_inv(d.x), safe_inv(d.y), safe_inv(d.z));
+  const f3 sinv = mk(s.x * inv.x, s.y * inv.y, s.z * inv.z);
   int sp = 0;  // the node to visit next stays in a scalar register; the other hit children go to stk
   uint32_t next = (m.n > 0 && __any(active)) ? 0u : 0xFFFFFFFFu;
   unsigned long long next_hm = 0ull;
@@ -1248,9 +1253,6 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
   }
 #endif
   BZR_PHASE(3)
-#if !BZR_TRAV_BUNDLE  // (the bundle walk ends with an empty stack and tests wide waves' nodes per lane itself)
-  const f3 inv = mk(safe_inv(d.x), safe_inv(d.y), safe_inv(d.z));
-  const f3 sinv = mk(s.x * inv.x, s.y * inv.y, s.z * inv.z);
   while (next != 0xFFFFFFFFu || sp > 0) {  // the per-lane walk
     const uint32_t node = next != 0xFFFFFFFFu ? next : __builtin_amdgcn_readfirstlane(stk[--sp]);
     next = 0xFFFFFFFFu;
@@ -1283,7 +1285,6 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
       }
     }
   }
-#endif
   // the always list (patches without a proven gate region, bvh.cpp): gate-tested for every active ray
   BZR_PHASE(4)
   if (m.n_always && __any(active)) {
