@@ -2443,11 +2443,18 @@ __device__ __forceinline__ uint32_t trace_tile(uint32_t b, uint32_t nblocks) {
 #ifndef BZR_TRACE_SCHED_REFRESH
 #define BZR_TRACE_SCHED_REFRESH 16
 #endif
+// BZR_TRACE_SCHED_OCT (default 4): cost classes per octave of cycles (1, 2 or 4).  Within a class the tiles keep
+// roughly their input order (each k_sched_place block reserves its tiles' places in dispatch order), so coarser
+// classes keep more of the input order's locality.
+#ifndef BZR_TRACE_SCHED_OCT
+#define BZR_TRACE_SCHED_OCT 4
+#endif
 constexpr uint32_t kSchedBins = 128, kSchedMinTiles = 2048, kSchedThreads = 256;
 __device__ __forceinline__ uint32_t sched_bin(unsigned long long cycles) {
   const uint32_t c = static_cast<uint32_t>(cycles > 0xFFFFFFFFull ? 0xFFFFFFFFull : cycles) | 4u;
   const uint32_t lg = 31u - __clz(c);                           // >= 2
-  const uint32_t key = 4u * lg + ((c >> (lg - 2u)) & 3u);       // 4 classes per octave, 8..127
+  constexpr uint32_t kSub = BZR_TRACE_SCHED_OCT == 4 ? 2u : (BZR_TRACE_SCHED_OCT == 2 ? 1u : 0u);
+  const uint32_t key = 4u * lg + (((c >> (lg - 2u)) & 3u) >> (2u - kSub) << (2u - kSub));  // <= 127
   return kSchedBins - 1u - key;                                  // bin 0 = the longest
 }
 // tiles per bin (hist zeroed by the previous k_sched_scan, or at allocation)
