@@ -10,6 +10,11 @@ if [ -z "$GRAFT_REPO_ROOT" ] || [ ! -f "$GRAFT_REPO_ROOT/bench.py" ]; then
   exit 2
 fi
 R="$GRAFT_REPO_ROOT"; OUT="$R/gpurun_out/${TAG:-prof}"; mkdir -p "$OUT"; cd /tmp && export TMPDIR=/tmp
+# the rocprofv3 databases are large: delete them however the script ends, or a failed pass leaves them behind and
+# the pulled gpurun_out/ outgrows gpurun's merge limit (round 4's "prof rc=2 with an empty prof.log": the passes'
+# own logs, under $OUT, never came back)
+trap 'find "$OUT" -name "*.db" -delete 2>/dev/null' EXIT
+echo "prof_run.sh: outputs under $OUT (each pass: <name>.log; summary.txt)"
 # --inflight 1: each launch runs alone, so the trace's per-launch durations compare with bench.py's
 # roofline.avg_launch_ms (measured on serialized launches); with two frames in flight the launches overlap.
 B="$R/bench.py --steps ${PROF_STEPS:-5} --warmup 1 --prewarm-s 0.3 --cpu-baseline off --inflight 1 ${BENCH:-}"
