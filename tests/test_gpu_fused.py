@@ -153,3 +153,30 @@ def test_full_size_fused_equals_staged(bzr, name, side):
         torch.cuda.synchronize()
         assert torch.equal(f.view(torch.int32), s.view(torch.int32))
         assert int((f[11].view(torch.int32) == 4).sum()) > rays.shape[1] // 10  # hits (what == intersect)
+
+
+def test_cost_ordered_dispatch_keeps_the_bits(bzr, cfg2_lens):
+    """k_trace's cost-ordered dispatch: a context's repeated fused calls of one size run
+    their tiles longest-first from the previous calls' wave durations (the order is built on the first call of
+    a size and rebuilt every 16 calls).  Calls 1..40 of one size, with calls of another size and an intersect
+    call interleaved (size switches drop the order), must all equal the brute-force scan bit for bit."""
+    import torch
+
+    ctx = bzr.Context(0)  # a fresh context: no order yet
+    dm = bzr.DeviceMesh(ctx, cfg2_lens)
+    rays = torch.from_numpy(grid_rays(CONFIGS["cfg2"], side=512)).cuda()      # 4096 tiles (> 2048: ordered)
+    other = torch.from_numpy(grid_rays(CONFIGS["cfg2"], side=384)).cuda()     # 2304 tiles
+    want = [t.cpu().numpy() for t in bzr.trace_chain(ctx, [dm], [1.3], rays, mode=bzr.ACCEL_NONE)]
+    want_o = [t.cpu().numpy() for t in bzr.trace_chain(ctx, [dm], [1.3], other, mode=bzr.ACCEL_NONE)]
+    want_h = bzr.intersect(ctx, dm, rays, mode=bzr.ACCEL_NONE).cpu().numpy()
+    for k in range(40):
+        got = bzr.trace_chain(ctx, [dm], [1.3], rays, mode=bzr.PIPELINE_FUSED)
+        for g, w in zip(got, want):
+            assert np.array_equal(u32(g.cpu().numpy()), u32(w)), k
+        if k in (5, 22):
+            got = bzr.trace_chain(ctx, [dm], [1.3], other, mode=bzr.PIPELINE_FUSED)
+            for g, w in zip(got, want_o):
+                assert np.array_equal(u32(g.cpu().numpy()), u32(w)), ("other size", k)
+        if k == 30:
+            h = bzr.intersect(ctx, dm, rays, mode=bzr.PIPELINE_FUSED).cpu().numpy()
+            assert np.array_equal(u32(h), u32(want_h))
