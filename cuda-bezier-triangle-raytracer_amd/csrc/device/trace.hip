@@ -1613,6 +1613,11 @@ __device__ __forceinline__ void flush_follow(uint32_t *buf, uint32_t &nf, uint32
 #define BZR_NEWTON_WPE 8
 #endif
 #define BZR_NEWTON_ATTR __attribute__((amdgpu_waves_per_eu(BZR_NEWTON_WPE)))
+// BZR_NEWTON_PREFETCH (A/B knob, default 0): k_newton loads a chunk's rays while the previous chunk computes
+// (and the pair records two chunks ahead) instead of at the chunk's start.
+#ifndef BZR_NEWTON_PREFETCH
+#define BZR_NEWTON_PREFETCH 0
+#endif
 template <bool kFast>
 __global__ __launch_bounds__(kBlock) BZR_NEWTON_ATTR void k_newton(const float *__restrict__ full,
                                                    const unsigned long long *__restrict__ total,
@@ -1635,15 +1640,31 @@ __global__ __launch_bounds__(kBlock) BZR_NEWTON_ATTR void k_newton(const float *
   q = __builtin_amdgcn_readfirstlane(q);
   uint2 pr = make_uint2(kNoPair, 0u);
   if (q < D) pr = pairs[q * 64u + lane];
+#if BZR_NEWTON_PREFETCH
+  // two-deep pipeline: this chunk's rays were loaded during the previous chunk, the next chunk's pair records
+  // two chunks ahead
+  f3 ns = mk(0.0f, 0.0f, 0.0f), nd = ns;
+  if (q < D && pr.x != kNoPair) load_pair_ray(aos, rays, ld, off, pr.x & kRayMask, ns, nd);
+  uint2 pr2 = make_uint2(kNoPair, 0u);
+  if (q + W < D) pr2 = pairs[(q + W) * 64u + lane];
+#endif
   for (; q < D; q += W) {
     const uint32_t p = q * 64u + lane;
     const bool todo = pr.x != kNoPair;
     const uint32_t ray = pr.x & kRayMask, j = pr.x >> 26;
     const uint32_t b = __builtin_amdgcn_readfirstlane(pr.y);  // the chunk's patch (lane 0 is a real pair)
+#if BZR_NEWTON_PREFETCH
+    const f3 s = ns, d = nd;
+    const uint32_t qn = q + W;
+    pr = pr2;  // the next chunk's pairs (loaded a chunk ago): its rays now, its successor's pairs too
+    if (qn < D && pr.x != kNoPair) load_pair_ray(aos, rays, ld, off, pr.x & kRayMask, ns, nd);
+    if (qn + W < D) pr2 = pairs[(qn + W) * 64u + lane];
+#else
     f3 s = mk(0.0f, 0.0f, 0.0f), d = s;
     if (todo) load_pair_ray(aos, rays, ld, off, ray, s, d);  // pairs of one patch: mostly neighbouring rays
     const uint32_t qn = q + W;  // prefetch the next chunk's pair records
     if (qn < D) pr = pairs[qn * 64u + lane];
+#endif
     bool is_fol = false;
     const auto pa = uniform_patch(full, b);
     if (todo) {
