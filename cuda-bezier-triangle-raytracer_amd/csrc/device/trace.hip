@@ -1614,7 +1614,9 @@ __device__ __forceinline__ void flush_follow(uint32_t *buf, uint32_t &nf, uint32
 #endif
 #define BZR_NEWTON_ATTR __attribute__((amdgpu_waves_per_eu(BZR_NEWTON_WPE)))
 // BZR_NEWTON_PREFETCH (A/B knob, default 0): k_newton loads a chunk's rays while the previous chunk computes
-// (and the pair records two chunks ahead) instead of at the chunk's start.
+// (and the pair records two chunks ahead) instead of at the chunk's start.  61 instead of 54 VGPRs, still 8
+// waves: cfg5 k_newton 4.32 -> 4.26 ms per frame, frames within noise; cfg3 frames -3 % (noisy)
+// (profiles/r05_ab_newton_prefetch.jsonl): the eight waves per SIMD already hide the gathers.  Not kept.
 #ifndef BZR_NEWTON_PREFETCH
 #define BZR_NEWTON_PREFETCH 0
 #endif
