@@ -1746,12 +1746,38 @@ template <int kMode, bool kFast>
 #else
 #define BZR_RESOLVE_ATTR
 #endif
+// BZR_FINISH_NORAY (A/B knob, default 0): the intersect segments' k_finish reads no ray -- a BezierIntersection
+// needs none -- and the overflow rays (whose winner k_finish would evaluate again, with the ray) are emitted by
+// k_finish_ovf just before it; 24 B per ray less of an HBM-bound kernel, one launch more per chunk.
+#ifndef BZR_FINISH_NORAY
+#define BZR_FINISH_NORAY 0
+#endif
 __global__ __launch_bounds__(kBlock) BZR_FINISH_ATTR void k_finish(MeshView m, const float *rays, uint32_t ld, uint32_t off, uint32_t n,
                                                    Work w, Out o) {
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   if (blockIdx.x == 0 && threadIdx.x < 4) w.ctr[threadIdx.x] = 0u;  // last reader of the counters this segment
   if (i >= n) return;
   const uint32_t gi = off + i;
+  if constexpr (kMode == kModeHits && BZR_FINISH_NORAY) {
+    if (w.count[i] > kMaxCand) return;  // an overflow ray: k_finish_ovf emitted it
+    const unsigned long long k = w.key[i];
+    Hit h = no_hit();
+    uint32_t patch = 0xFFFFFFFFu;
+    if (k != ~0ull) {
+      const size_t sl = (size_t)(static_cast<uint32_t>(k) & 63u) * n + i;
+      const float4 *r = reinterpret_cast<const float4 *>(w.slot) + 3 * sl;
+      const float4 r0 = r[0], r1 = r[1], r2 = r[2];
+      h.t = r0.x;
+      h.point = mk(r0.y, r0.z, r0.w);
+      h.cs = r1.x;
+      h.bary = mk(r1.y, r1.z, r1.w);
+      h.normal = mk(r2.x, r2.y, r2.z);
+      h.what = kIntersect;
+      patch = __float_as_uint(r2.w);
+    }
+    store_hit(o.hits, ld, gi, h, patch);
+    return;
+  }
   if (kMode == kModeStage && !o.first && o.status[gi] == BZR_RR_NONE) return;
   // the ray is loaded unconditionally: making the load depend on w.count (an intersect chunk's hits need it
   // only for an overflow ray) serialises the two reads and measured slower (cfg3 k_finish 0.059 -> 0.069 ms,
@@ -1778,6 +1804,24 @@ __global__ __launch_bounds__(kBlock) BZR_FINISH_ATTR void k_finish(MeshView m, c
     patch = __float_as_uint(r2.w);
   }
   emit<kMode>(o, ld, gi, s, d, h, patch);
+}
+
+// BZR_FINISH_NORAY: the overflow rays of an intersect segment (the w.ovf list), emitted before k_finish (which
+// clears the counters and skips these rays): their winner -- k_resolve's full-scan key -- evaluated again.
+template <bool kFast>
+__global__ __launch_bounds__(kBlock) void k_finish_ovf(MeshView m, const float *rays, uint32_t ld, uint32_t off, Work w,
+                                                       Out o) {
+  const uint32_t V = __builtin_amdgcn_readfirstlane(w.ctr[1]);
+  for (uint32_t q = blockIdx.x * kBlock + threadIdx.x; q < V; q += gridDim.x * kBlock) {
+    const uint32_t i = w.ovf[q], gi = off + i;
+    f3 s, d;
+    load_ray(rays, ld, gi, s, d);
+    Hit h = no_hit();
+    uint32_t patch = 0xFFFFFFFFu;
+    const unsigned long long k = w.key[i];
+    if (k != ~0ull) h = evaluate_patch<kFast>(m, static_cast<uint32_t>(k), s, d, patch);
+    store_hit(o.hits, ld, gi, h, patch);
+  }
 }
 
 // The rays k_traverse could not take: the reference's full in-order scan, split into
@@ -2942,6 +2986,8 @@ bzr_status run_culled(bzr_ctx *ctx, const MeshView &mv, const float *rays, uint3
   }
   if (ctx->counting && ctx->counters)  // before k_finish, which clears the counters
     hipLaunchKernelGGL(k_count, dim3(1), dim3(64), 0, ctx->stream, w, nb, ctx->counters);
+  if (kMode == kModeHits && BZR_FINISH_NORAY)  // the overflow rays first (k_finish clears their count)
+    launch(ctx, BZR_KERNEL_FINISH, k_finish_ovf<kFast>, dim3(16), mv, rays, ld, off, w, o);
   launch(ctx, BZR_KERNEL_FINISH, k_finish<kMode, kFast>, dim3(grid_for(n)), mv, rays, ld, off, n, w, o);
   BZR_HIP(hipGetLastError());
   ctx->zero_ctr = w.ctr;  // k_place cleared the histogram, k_finish the counters
