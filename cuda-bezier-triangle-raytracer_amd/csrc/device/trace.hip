@@ -1748,7 +1748,9 @@ template <int kMode, bool kFast>
 #endif
 // BZR_FINISH_NORAY (A/B knob, default 0): the intersect segments' k_finish reads no ray -- a BezierIntersection
 // needs none -- and the overflow rays (whose winner k_finish would evaluate again, with the ray) are emitted by
-// k_finish_ovf just before it; 24 B per ray less of an HBM-bound kernel, one launch more per chunk.
+// k_finish_ovf just before it; 24 B per ray less of an HBM-bound kernel, one launch more per chunk.  cfg5 frames
+// +0.6 %, cfg3 -0.6 to -1 % with frames in flight, the finish pair slower on lone frames
+// (profiles/r05_ab_finish_noray.jsonl): not kept.
 #ifndef BZR_FINISH_NORAY
 #define BZR_FINISH_NORAY 0
 #endif
