@@ -2113,7 +2113,8 @@ __device__ __forceinline__ Hit parked(TraceLds<kMode> &L, uint32_t lane) {
 // One BezierMesh::intersect for the wave's active lanes; the winner is left in `best` / L.hit.
 template <int kMode, bool kFast, bool kCount>
 __device__ __forceinline__ void trace_segment(const MeshView &m, f3 s, f3 d, bool act, unsigned long long &best,
-                                              TraceLds<kMode> &L, uint32_t lane, TraceCtr &ctr) {
+                                              TraceLds<kMode> &L, uint32_t lane, TraceCtr &ctr,
+                                              uint32_t *pflag = nullptr) {
   constexpr bool kPark = TraceWords<kMode>::kPark > 0;
   constexpr uint32_t kNo = 0xFFFFFFFFu;
   constexpr int kCap = TraceWords<kMode>::kStackCap;
@@ -2164,8 +2165,19 @@ __device__ __forceinline__ void trace_segment(const MeshView &m, f3 s, f3 d, boo
     bwalk = true;
   }
 #endif
+#if BZR_TRACE_PAIRSYNC
+  bool seg_done = false;  // this wave has no batch left in the segment (its partner may)
+#endif
   for (;;) {
     uint32_t ne = 0;  // collected leaves (uniform)
+#if BZR_TRACE_PAIRSYNC
+    // meeting point A: where two-wave lending would swap the waves' entry lists; the loop
+    // ends once both waves are done, and a done wave keeps meeting its partner with empty batches
+    if (lane == 0u) pflag[threadIdx.x >> 6] = seg_done ? 1u : 0u;
+    __syncthreads();
+    if (pflag[0] && pflag[1]) break;
+    if (!seg_done) {
+#endif
 #if BZR_TRACE_PRIO
     __builtin_amdgcn_s_setprio(BZR_TRACE_PRIO);  // the walk is latency-bound: issue it ahead of Newton passes
 #endif
@@ -2338,8 +2350,17 @@ __device__ __forceinline__ void trace_segment(const MeshView &m, f3 s, f3 d, boo
       }
     }
     if (ne == 0u) {  // tree done: the reference's in-order scan for the lanes that could not use it
+#if BZR_TRACE_PAIRSYNC
+#define BZR_SEG_END       \
+  {                       \
+    seg_done = true;      \
+    goto pair_b;          \
+  }
+#else
+#define BZR_SEG_END break;
+#endif
       if (scan == kNo) {
-        if (!__any(ovf)) break;
+        if (!__any(ovf)) BZR_SEG_END
         scan = 0;
         if (kCount) ctr.ovf += popc64(__ballot(ovf));
       }
@@ -2349,7 +2370,8 @@ __device__ __forceinline__ void trace_segment(const MeshView &m, f3 s, f3 d, boo
         pass = ovf && planar_gate(g[0], g[1], g[2], g[3], s, d);
         if (__any(pass)) break;
       }
-      if (scan >= m.n) break;
+      if (scan >= m.n) BZR_SEG_END
+#undef BZR_SEG_END
       const unsigned long long pm = __ballot(pass);
       if (lane == 0u) {
         L.eid[0] = scan;
@@ -2358,6 +2380,12 @@ __device__ __forceinline__ void trace_segment(const MeshView &m, f3 s, f3 d, boo
       ne = 1;
       ++scan;
     }
+#if BZR_TRACE_PAIRSYNC
+    }  // !seg_done
+  pair_b:
+    __syncthreads();  // meeting point B: where lending would hand the borrowed lanes' results back
+    if (seg_done) ne = 0u;
+#endif
     // the collected leaves' passes, in order
 #if BZR_TRACE_PRIO
     __builtin_amdgcn_s_setprio(0);
@@ -2481,8 +2509,14 @@ struct TraceJob {
 #endif
 // Threads per k_trace block (BZR_TRACE_BLOCK): its waves share nothing but the CU, so one-wave blocks let
 // a finished wave be replaced at once (waves run 1-4 segments; 64 vs 256: cfg4 -3 %, cfg5 -7 %).
+// BZR_TRACE_PAIRSYNC (diagnostic A/B, default 0): two-wave k_trace blocks whose waves meet twice per collected
+// batch, as lane lending between them would need, with nothing lent: the measured cost of
+// the pairing alone, against scripts/pair_sim.py's bound on what lending could save.
+#ifndef BZR_TRACE_PAIRSYNC
+#define BZR_TRACE_PAIRSYNC 0
+#endif
 #ifndef BZR_TRACE_BLOCK
-#define BZR_TRACE_BLOCK 64
+#define BZR_TRACE_BLOCK (BZR_TRACE_PAIRSYNC ? 128 : 64)
 #endif
 constexpr int kTraceBlock = BZR_TRACE_BLOCK, kTraceWaves = kTraceBlock / 64;
 // Which 64-ray tile block b takes (BZR_TRACE_XCD): 0 = the dispatch order itself (XCD x gets every 8th
@@ -2573,6 +2607,12 @@ template <int kMode, bool kFast, bool kCount>
 __global__ __launch_bounds__(kTraceBlock) BZR_TRACE_ATTR void k_trace(LensSet lenses, TraceJob job,
                                                                       unsigned long long *__restrict__ counters) {
   __shared__ TraceLds<kMode> lds[kTraceWaves];
+#if BZR_TRACE_PAIRSYNC
+  static_assert(kTraceWaves == 2, "BZR_TRACE_PAIRSYNC pairs the two waves of a 128-thread block");
+  __shared__ uint32_t pflag[2];
+#else
+  uint32_t *const pflag = nullptr;
+#endif
   const uint32_t lane = threadIdx.x & 63u;
   TraceLds<kMode> &L = lds[threadIdx.x >> 6];
   const uint32_t tile = job.order ? job.order[blockIdx.x] : trace_tile(blockIdx.x, gridDim.x);
@@ -2589,10 +2629,10 @@ __global__ __launch_bounds__(kTraceBlock) BZR_TRACE_ATTR void k_trace(LensSet le
   const uint32_t nseg = kMode == kModeStage ? 2u * lenses.count : 1u;
   uint32_t st = BZR_RR_NONE, seg = 0;
   for (uint32_t k = 0; k < nseg; ++k) {
-    if (!__any(alive)) break;
+    if (!BZR_TRACE_PAIRSYNC && !__any(alive)) break;  // (paired waves both run every segment: same meetings)
     const MeshView &m = lenses.lens[k >> 1];
     unsigned long long best;
-    trace_segment<kMode, kFast, kCount>(m, s, d, alive, best, L, lane, ctr);
+    trace_segment<kMode, kFast, kCount>(m, s, d, alive, best, L, lane, ctr, pflag);
     if (kCount) ctr.segments += popc64(__ballot(alive));
     Hit h = no_hit();
     uint32_t patch = 0xFFFFFFFFu;
