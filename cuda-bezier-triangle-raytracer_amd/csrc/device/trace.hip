@@ -2511,7 +2511,8 @@ struct TraceJob {
 // a finished wave be replaced at once (waves run 1-4 segments; 64 vs 256: cfg4 -3 %, cfg5 -7 %).
 // BZR_TRACE_PAIRSYNC (diagnostic A/B, default 0): two-wave k_trace blocks whose waves meet twice per collected
 // batch, as lane lending between them would need, with nothing lent: the measured cost of
-// the pairing alone, against scripts/pair_sim.py's bound on what lending could save.
+// the pairing alone, against scripts/pair_sim.py's bound on what lending could save.  Same bits
+// and passes; cfg4 -8.4 %, cfg2 -8.6 % (profiles/r05_ab_pairsync.jsonl) against <= ~2 % lending could recover.
 #ifndef BZR_TRACE_PAIRSYNC
 #define BZR_TRACE_PAIRSYNC 0
 #endif
