@@ -36,6 +36,7 @@ MODE_PARITY, MODE_FAST = 0, 2
 ACCEL_NONE = 4  # brute-force scan (A/B against the default BVH-culled path)
 PIPELINE_STAGED = 8  # the culled path as separate kernels (traverse, bucket, Newton, resolve, finish)
 PIPELINE_FUSED = 16  # the culled path as one k_trace kernel (default for dense batches; see include/bzr.h)
+RAYS_AOS = 32  # rays / out_rays as [n, 6] records (the reference's Ray layout), transposed on the device
 WHAT_FOLLOW0, WHAT_FOLLOW1, WHAT_FOLLOW2, WHAT_NONE, WHAT_INTERSECT = 0, 1, 2, 3, 4
 LIMIT_THIS, LIMIT_NONE = 0, 1
 RR_NONE, RR_INSIDE, RR_OUTSIDE = 0, 1, 2
@@ -302,27 +303,34 @@ class DeviceMesh:
             pass
 
 
-def _n_of(rays) -> int:
+def _n_of(rays, mode=0) -> int:
+    """Rays in a batch: [6, n] rows, or [n, 6] records when mode has RAYS_AOS."""
     shape = tuple(rays.shape)
+    if mode & RAYS_AOS:
+        if len(shape) != 2 or shape[1] != 6:
+            raise BzrError(f"RAYS_AOS rays must be [n, 6], got {shape}")
+        return int(shape[0])
     if len(shape) != 2 or shape[0] != 6:
         raise BzrError(f"rays must be [6, n], got {shape}")
     return int(shape[1])
 
 
-def _empty_like(rays, rows, dtype):
-    n = _n_of(rays)
+def _empty_like(rays, rows, dtype, mode=0):
+    n = _n_of(rays, mode)
+    shape = ((n, 6) if mode & RAYS_AOS else (6, n)) if rows == 6 else ((rows, n) if rows else (n,))
     if _is_tensor(rays):
         import torch
 
         tdt = {np.float32: torch.float32, np.uint32: torch.int32}[dtype]
-        return torch.empty((rows, n) if rows else (n,), dtype=tdt, device=rays.device)
-    return np.empty((rows, n) if rows else (n,), dtype=dtype)
+        return torch.empty(shape, dtype=tdt, device=rays.device)
+    return np.empty(shape, dtype=dtype)
 
 
 def intersect(ctx: Context, mesh: DeviceMesh, rays, out=None, mode=MODE_PARITY):
-    """BezierMesh::intersect over a batch -> hits [13, n].  mode |= ACCEL_NONE for the brute-force scan."""
-    n = _n_of(rays)
-    out = _empty_like(rays, HIT_FIELDS, np.float32) if out is None else out
+    """BezierMesh::intersect over a batch -> hits [13, n].  mode |= ACCEL_NONE for the brute-force scan; mode |=
+    RAYS_AOS for [n, 6] ray records."""
+    n = _n_of(rays, mode)
+    out = _empty_like(rays, HIT_FIELDS, np.float32, mode) if out is None else out
     r, o = _Buf(rays, np.float32), _Buf(out, np.float32, True)
     res = _residency(r, o)
     with _stream_for(ctx, res):
@@ -344,10 +352,10 @@ def patch_intersect(ctx: Context, mesh: DeviceMesh, patch_index, limit, rays, ou
 
 def refract(ctx: Context, mesh: DeviceMesh, ri: float, rays, expected=None, expected_all=RR_INSIDE,
             out_rays=None, out_status=None, mode=MODE_PARITY):
-    """BezierLens::refract over a batch -> (rays [6, n], status [n])."""
-    n = _n_of(rays)
-    out_rays = _empty_like(rays, 6, np.float32) if out_rays is None else out_rays
-    out_status = _empty_like(rays, 0, np.uint32) if out_status is None else out_status
+    """BezierLens::refract over a batch -> (rays [6, n], status [n]); RAYS_AOS in mode: rays [n, 6] both ways."""
+    n = _n_of(rays, mode)
+    out_rays = _empty_like(rays, 6, np.float32, mode) if out_rays is None else out_rays
+    out_status = _empty_like(rays, 0, np.uint32, mode) if out_status is None else out_status
     r, e = _Buf(rays, np.float32), _Buf(expected, np.uint32)
     o, s = _Buf(out_rays, np.float32, True), _Buf(out_status, np.uint32, True)
     res = _residency(r, o, s, *([e] if expected is not None else []))
@@ -358,14 +366,15 @@ def refract(ctx: Context, mesh: DeviceMesh, ri: float, rays, expected=None, expe
 
 
 def trace_chain(ctx: Context, lenses, ri, rays, out_rays=None, out_status=None, out_segments=None, mode=MODE_PARITY):
-    """Refraction chain through `lenses` (list of DeviceMesh) -> (rays [6, n], status [n], segments [n])."""
-    n = _n_of(rays)
+    """Refraction chain through `lenses` (list of DeviceMesh) -> (rays [6, n], status [n], segments [n]);
+    RAYS_AOS in mode: rays [n, 6] both ways."""
+    n = _n_of(rays, mode)
     nl = len(lenses)
     handles = (_P * nl)(*[m.handle for m in lenses])
     ris = (_F * nl)(*[float(x) for x in ri])
-    out_rays = _empty_like(rays, 6, np.float32) if out_rays is None else out_rays
-    out_status = _empty_like(rays, 0, np.uint32) if out_status is None else out_status
-    out_segments = _empty_like(rays, 0, np.uint32) if out_segments is None else out_segments
+    out_rays = _empty_like(rays, 6, np.float32, mode) if out_rays is None else out_rays
+    out_status = _empty_like(rays, 0, np.uint32, mode) if out_status is None else out_status
+    out_segments = _empty_like(rays, 0, np.uint32, mode) if out_segments is None else out_segments
     r = _Buf(rays, np.float32)
     o, s, g = _Buf(out_rays, np.float32, True), _Buf(out_status, np.uint32, True), _Buf(out_segments, np.uint32, True)
     res = _residency(r, o, s, g)
@@ -411,14 +420,15 @@ def trace_tiled(ctxs, lenses, ri, rays, tile_rays=4096, mode=MODE_PARITY, out=No
     """bzr_trace_tiled: the chain over several contexts (one per device) from one process, gathered to
     ctxs[0]'s device on the device side.  `lenses[d]` is the list of DeviceMesh living on ctxs[d]; rays
     [6, n] ordered tile-major, a host array or a tensor on ctxs[0]'s device (then the outputs are tensors
-    there).  -> (rays [6, n], status [n], segments [n]) in input order."""
+    there).  -> (rays [6, n], status [n], segments [n]) in input order (RAYS_AOS in mode: rays [n, 6] both ways)."""
     nc, nl = len(ctxs), len(ri)
     if len(lenses) != nc or any(len(ls) != nl for ls in lenses):
         raise ValueError("lenses must hold one list of len(ri) meshes per context")
     r = _Buf(rays, np.float32)
-    n = _n_of(rays)
+    n = _n_of(rays, mode)
     if out is None:
-        out = (_empty_like(rays, 6, np.float32), _empty_like(rays, 0, np.uint32), _empty_like(rays, 0, np.uint32))
+        out = (_empty_like(rays, 6, np.float32, mode), _empty_like(rays, 0, np.uint32, mode),
+               _empty_like(rays, 0, np.uint32, mode))
     o, s_, g = _Buf(out[0], np.float32, True), _Buf(out[1], np.uint32, True), _Buf(out[2], np.uint32, True)
     res = _residency(r, o, s_, g)
     cs = (_P * nc)(*[c.handle for c in ctxs])
@@ -460,13 +470,16 @@ class TiledPlan:
         _check(lib().bzr_tiled_info(self.handle, ctypes.byref(t), share.ctypes.data, ctypes.byref(npad)))
         return int(t.value), share, int(npad.value)
 
-    def set_rays(self, rays):
+    def set_rays(self, rays, mode=0):
+        """The frame's rays [6, n] (or [n, 6] records with mode RAYS_AOS), host array or tensor on device 0."""
+        if _n_of(rays, mode) != self.n:
+            raise BzrError(f"set_rays: {_n_of(rays, mode)} rays for a plan of {self.n}")
         r = _Buf(rays, np.float32)
         if r.device:
             import torch
 
             torch.cuda.current_stream(self.ctxs[0][0].device).synchronize()
-        _check(lib().bzr_tiled_set_rays(self.handle, r.ptr, DEVICE_PTRS if r.device else HOST_PTRS))
+        _check(lib().bzr_tiled_set_rays(self.handle, r.ptr, (DEVICE_PTRS if r.device else HOST_PTRS) | (mode & RAYS_AOS)))
 
     def trace(self, lenses, ri, out_rays, out_status, out_segments=None, mode=MODE_PARITY):
         """One frame; lenses[d] = device d's DeviceMesh list.  Device tensors (on device 0): queued, ready on

@@ -46,3 +46,7 @@ struct bzr_ctx {
   uint32_t sched_waves = 0;  // waves of the call whose order is ready (0: none)
   uint32_t sched_calls = 0;  // calls since the order was first built for this size (rebuilt every BZR_TRACE_SCHED_REFRESH)
 };
+
+// BZR_RAYS_AOS (frame_pack.hip): n rays between the reference's [n][6] records and the kernels' [6][n] rows,
+// device to device on `stream` (to_soa: src AoS -> dst rows; else rows -> AoS).  src and dst must not overlap.
+hipError_t bzr_rays_relayout(hipStream_t stream, const float *src, float *dst, uint32_t n, bool to_soa);

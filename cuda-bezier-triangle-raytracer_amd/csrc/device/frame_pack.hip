@@ -133,12 +133,60 @@ __global__ __launch_bounds__(kPackThreads) void k_compact_scatter(const float *_
   }
 }
 
+// BZR_RAYS_AOS: the reference's Ray records ([n][6]: start xyz, direction xyz, 24 bytes) <-> the kernels'
+// rows ([6][n]).  A block moves 256 rays' 6 KB through LDS so that both sides are read and written
+// contiguously (6 coalesced rounds each); stride 6 in LDS is a 2-way bank conflict.  HBM-bound: 48 bytes
+// per ray.
+constexpr uint32_t kRayWords = 6;
+__global__ __launch_bounds__(kPackThreads) void k_rays_aos_to_soa(const float *__restrict__ aos, uint32_t n,
+                                                                  float *__restrict__ soa) {
+  __shared__ float t[kRayWords * kPackThreads];
+  const size_t r0 = (size_t)blockIdx.x * kPackThreads;
+  const uint32_t m = static_cast<uint32_t>(min<size_t>(kPackThreads, n - r0));
+#pragma unroll
+  for (uint32_t k = 0; k < kRayWords; ++k) {
+    const uint32_t w = k * kPackThreads + threadIdx.x;
+    if (w < kRayWords * m) t[w] = aos[kRayWords * r0 + w];
+  }
+  __syncthreads();
+  if (threadIdx.x < m) {
+#pragma unroll
+    for (uint32_t k = 0; k < kRayWords; ++k) soa[(size_t)k * n + r0 + threadIdx.x] = t[kRayWords * threadIdx.x + k];
+  }
+}
+__global__ __launch_bounds__(kPackThreads) void k_rays_soa_to_aos(const float *__restrict__ soa, uint32_t n,
+                                                                  float *__restrict__ aos) {
+  __shared__ float t[kRayWords * kPackThreads];
+  const size_t r0 = (size_t)blockIdx.x * kPackThreads;
+  const uint32_t m = static_cast<uint32_t>(min<size_t>(kPackThreads, n - r0));
+  if (threadIdx.x < m) {
+#pragma unroll
+    for (uint32_t k = 0; k < kRayWords; ++k) t[kRayWords * threadIdx.x + k] = soa[(size_t)k * n + r0 + threadIdx.x];
+  }
+  __syncthreads();
+#pragma unroll
+  for (uint32_t k = 0; k < kRayWords; ++k) {
+    const uint32_t w = k * kPackThreads + threadIdx.x;
+    if (w < kRayWords * m) aos[kRayWords * r0 + w] = t[w];
+  }
+}
+
 bzr_status fail(bzr_status s, const std::string &msg) {
   bzr_internal_set_error(msg.c_str());
   return s;
 }
 
 }  // namespace
+
+hipError_t bzr_rays_relayout(hipStream_t stream, const float *src, float *dst, uint32_t n, bool to_soa) {
+  if (n == 0) return hipSuccess;
+  const dim3 grid((n + kPackThreads - 1) / kPackThreads);
+  if (to_soa)
+    hipLaunchKernelGGL(k_rays_aos_to_soa, grid, dim3(kPackThreads), 0, stream, src, n, dst);
+  else
+    hipLaunchKernelGGL(k_rays_soa_to_aos, grid, dim3(kPackThreads), 0, stream, src, n, dst);
+  return hipGetLastError();
+}
 
 extern "C" bzr_status bzr_pack_frame(bzr_ctx *ctx, int32_t layout, const float *rays_soa, const uint32_t *status,
                                      const uint32_t *segments, uint32_t n, uint32_t npad, uint32_t cap, void *packed) {

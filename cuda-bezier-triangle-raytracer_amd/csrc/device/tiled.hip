@@ -243,6 +243,8 @@ struct bzr_tiled {
     // gather stream of d, on dev[d]; peer: gstream[0], on dev[0]) -- HIP records an event only on a stream of
     // the event's own device
     std::vector<hipEvent_t> sent_ev;
+    float *rows = nullptr;           // BZR_RAYS_AOS: device 0, the frame's output rays [6][n] before they become
+                                     // records (per slot: a DIRECT frame writes them on its own slot stream)
     bool used = false;
   };
   std::vector<Slot> slot;
@@ -293,6 +295,7 @@ struct bzr_tiled {
         free_on(dev[d], s.packed[d]);
       }
       free_on(dev.empty() ? 0 : dev[0], s.recv);
+      free_on(dev.empty() ? 0 : dev[0], s.rows);
       for (hipEvent_t e : s.packed_ev) if (e) (void)hipEventDestroy(e);
       for (hipEvent_t e : s.sent_ev) if (e) (void)hipEventDestroy(e);
     }
@@ -463,7 +466,8 @@ extern "C" bzr_status bzr_tiled_share_rays(bzr_tiled *t, uint32_t d, float **ray
 extern "C" bzr_status bzr_tiled_set_rays(bzr_tiled *t, const float *rays, uint32_t flags) {
   if (!t) return fail(BZR_ERR_INVALID_ARGUMENT, "bzr_tiled_set_rays: null plan");
   if (!rays) return fail(BZR_ERR_INVALID_ARGUMENT, "bzr_tiled_set_rays: null rays");
-  if (flags & ~uint32_t(BZR_DEVICE_PTRS)) return fail(BZR_ERR_INVALID_ARGUMENT, "bzr_tiled_set_rays: unknown flags");
+  if (flags & ~uint32_t(BZR_DEVICE_PTRS | BZR_RAYS_AOS))
+    return fail(BZR_ERR_INVALID_ARGUMENT, "bzr_tiled_set_rays: unknown flags");
   // frames in flight read the share inputs and device 0's frame copy: they finish first
   if (bzr_status s = bzr_tiled_sync(t)) return s;
   t->prim_valid = false;
@@ -482,8 +486,19 @@ extern "C" bzr_status bzr_tiled_set_rays(bzr_tiled *t, const float *rays, uint32
     if (bzr_status s = alloc_on(t->dev[0], t->stage, stage_words)) return s;
   bzr_ctx *c0 = t->ctxs[0];
   DeviceGuard g(t->dev[0]);
-  const bool host = !(flags & BZR_DEVICE_PTRS);
-  TILED_HIP(hipMemcpyAsync(t->prim0, rays, bytes, host ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice, c0->stream));
+  const bool host = !(flags & BZR_DEVICE_PTRS), aos = (flags & BZR_RAYS_AOS) != 0;
+  if (aos) {  // [n][6] records: (copied to device 0's host_out staging, idle after the sync above and) transposed
+    const float *src = rays;
+    if (host) {
+      if (!t->host_out)
+        if (bzr_status s = alloc_on(t->dev[0], t->host_out, (size_t)8 * t->n)) return s;
+      TILED_HIP(hipMemcpyAsync(t->host_out, rays, bytes, hipMemcpyHostToDevice, c0->stream));
+      src = t->host_out;
+    }
+    TILED_HIP(bzr_rays_relayout(c0->stream, src, t->prim0, t->n, true));
+  } else {
+    TILED_HIP(hipMemcpyAsync(t->prim0, rays, bytes, host ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice, c0->stream));
+  }
   if (host) TILED_HIP(hipStreamSynchronize(c0->stream));  // the caller's host buffer has been read
   if (t->ndev > 1) {
     size_t off = 0;
@@ -566,7 +581,8 @@ extern "C" bzr_status bzr_tiled_trace(bzr_tiled *t, const bzr_mesh *const *lense
   if (!t) return fail(BZR_ERR_INVALID_ARGUMENT, "bzr_tiled_trace: null plan");
   if (!lenses || !ri || nlens == 0) return fail(BZR_ERR_INVALID_ARGUMENT, "bzr_tiled_trace: null lens list");
   if (!out_rays || !out_status) return fail(BZR_ERR_INVALID_ARGUMENT, "bzr_tiled_trace: null output");
-  const bool host = !(flags & BZR_DEVICE_PTRS);
+  const bool host = !(flags & BZR_DEVICE_PTRS), aos = (flags & BZR_RAYS_AOS) != 0;
+  const uint32_t cflags = (flags & ~uint32_t(BZR_RAYS_AOS)) | BZR_DEVICE_PTRS;  // the share inputs are rows
   if (t->layout == BZR_PACK_COMPACT && !t->prim_valid)
     return fail(BZR_ERR_INVALID_ARGUMENT, "bzr_tiled_trace: the compact layout needs the frame's rays through "
                                           "bzr_tiled_set_rays (device 0 returns the rays that never refracted)");
@@ -580,31 +596,45 @@ extern "C" bzr_status bzr_tiled_trace(bzr_tiled *t, const bzr_mesh *const *lense
       t->rays_seen[k] = t->rays_gen;
     }
   }
+  // where the frame's outputs land on device 0: the caller's device buffers, or staging -- host outputs in
+  // host_out ([6][n] rays, status, segments; copied back and waited for), BZR_RAYS_AOS rays in the slot's rows
+  // (then transposed into the caller's records, or into host_out's rays for a host caller)
+  float *o_rays = out_rays;
+  uint32_t *o_st = out_status, *o_seg = out_segments;
+  if (host) {
+    if (!t->host_out)
+      if (bzr_status st = alloc_on(t->dev[0], t->host_out, (size_t)8 * t->n)) return st;
+    o_rays = t->host_out;
+    o_st = reinterpret_cast<uint32_t *>(t->host_out + (size_t)6 * t->n);
+    o_seg = o_st + t->n;
+  }
+  if (aos) {
+    if (!sl.rows)
+      if (bzr_status st = alloc_on(t->dev[0], sl.rows, (size_t)6 * t->n)) return st;
+    o_rays = sl.rows;
+  }
+  // on device 0's stream that produced them: AoS records, then the copies back to the host
+  auto deliver = [&](hipStream_t os) -> bzr_status {
+    DeviceGuard g(t->dev[0]);
+    if (aos) TILED_HIP(bzr_rays_relayout(os, sl.rows, host ? t->host_out : out_rays, t->n, false));
+    if (!host) return BZR_OK;
+    TILED_HIP(hipMemcpyAsync(out_rays, t->host_out, (size_t)24 * t->n, hipMemcpyDeviceToHost, os));
+    TILED_HIP(hipMemcpyAsync(out_status, o_st, (size_t)4 * t->n, hipMemcpyDeviceToHost, os));
+    if (out_segments) TILED_HIP(hipMemcpyAsync(out_segments, o_seg, (size_t)4 * t->n, hipMemcpyDeviceToHost, os));
+    TILED_HIP(hipStreamSynchronize(os));
+    return BZR_OK;
+  };
   if (t->transport == BZR_GATHER_DIRECT) {
-    // one device: its share is the frame in frame order -- trace straight into the outputs (host outputs:
-    // device-0 staging, then copied back on the same stream), then hand the frame to the gather stream so
-    // bzr_tiled_stream keeps its meaning
+    // one device: its share is the frame in frame order -- trace straight into the outputs (or the staging
+    // above, delivered on the same stream), then hand the frame to the gather stream so bzr_tiled_stream keeps
+    // its meaning
     bzr_ctx *c = t->ctxs[s];
-    float *o_rays = out_rays;
-    uint32_t *o_st = out_status, *o_seg = out_segments;
-    if (host) {
-      if (!t->host_out)
-        if (bzr_status st = alloc_on(t->dev[0], t->host_out, (size_t)8 * t->n)) return st;
-      o_rays = t->host_out;
-      o_st = reinterpret_cast<uint32_t *>(t->host_out + (size_t)6 * t->n);
-      o_seg = o_st + t->n;
-    }
-    bzr_status st = bzr_trace_chain(c, lenses, ri, nlens, t->in[0], t->n, o_rays, o_st, o_seg, flags | BZR_DEVICE_PTRS);
+    bzr_status st = bzr_trace_chain(c, lenses, ri, nlens, t->in[0], t->n, o_rays, o_st, o_seg, cflags);
     if (st != BZR_OK) return fail(st, std::string("bzr_tiled_trace: ") + bzr_last_error());
     ++t->frames;
+    if (bzr_status e = deliver(c->stream)) return e;
+    if (host) return BZR_OK;
     DeviceGuard g(t->dev[0]);
-    if (host) {
-      TILED_HIP(hipMemcpyAsync(out_rays, o_rays, (size_t)24 * t->n, hipMemcpyDeviceToHost, c->stream));
-      TILED_HIP(hipMemcpyAsync(out_status, o_st, (size_t)4 * t->n, hipMemcpyDeviceToHost, c->stream));
-      if (out_segments) TILED_HIP(hipMemcpyAsync(out_segments, o_seg, (size_t)4 * t->n, hipMemcpyDeviceToHost, c->stream));
-      TILED_HIP(hipStreamSynchronize(c->stream));
-      return BZR_OK;
-    }
     TILED_HIP(hipEventRecord(sl.packed_ev[0], c->stream));
     TILED_HIP(hipStreamWaitEvent(t->gstream[0], sl.packed_ev[0], 0));
     return BZR_OK;
@@ -613,7 +643,7 @@ extern "C" bzr_status bzr_tiled_trace(bzr_tiled *t, const bzr_mesh *const *lense
     bzr_ctx *c = t->ctxs[(size_t)s * t->ndev + d];
     if (t->share[d]) {
       bzr_status st = bzr_trace_chain(c, lenses + (size_t)d * nlens, ri, nlens, t->in[d], t->share[d], sl.rays[d],
-                                      sl.status[d], sl.segments[d], flags | BZR_DEVICE_PTRS);
+                                      sl.status[d], sl.segments[d], cflags);
       if (st != BZR_OK) return fail(st, "bzr_tiled_trace: device " + std::to_string(d) + ": " + bzr_last_error());
     }
     DeviceGuard g(t->dev[d]);
@@ -628,32 +658,17 @@ extern "C" bzr_status bzr_tiled_trace(bzr_tiled *t, const bzr_mesh *const *lense
   }
   sl.used = true;
   ++t->frames;
-  float *o_rays = out_rays;
-  uint32_t *o_st = out_status, *o_seg = out_segments;
-  if (host) {  // unpack into device-0 staging, then copy out and wait
-    if (!t->host_out)
-      if (bzr_status st = alloc_on(t->dev[0], t->host_out, (size_t)8 * t->n)) return st;
-    o_rays = t->host_out;
-    o_st = reinterpret_cast<uint32_t *>(t->host_out + (size_t)6 * t->n);
-    o_seg = o_st + t->n;
-  }
   if (bzr_status st = gather_and_unpack(*t, sl, o_rays, o_st, o_seg)) return st;
-  if (host) {
+  if (bzr_status st = deliver(t->gstream[0])) return st;
+  if (host && t->layout == BZR_PACK_COMPACT) {  // a synchronous caller learns of an incomplete frame now
     DeviceGuard g(t->dev[0]);
-    hipStream_t gs = t->gstream[0];
-    TILED_HIP(hipMemcpyAsync(out_rays, o_rays, (size_t)24 * t->n, hipMemcpyDeviceToHost, gs));
-    TILED_HIP(hipMemcpyAsync(out_status, o_st, (size_t)4 * t->n, hipMemcpyDeviceToHost, gs));
-    if (out_segments) TILED_HIP(hipMemcpyAsync(out_segments, o_seg, (size_t)4 * t->n, hipMemcpyDeviceToHost, gs));
-    TILED_HIP(hipStreamSynchronize(gs));
-    if (t->layout == BZR_PACK_COMPACT) {  // a synchronous caller learns of an incomplete frame now
-      uint32_t *flag = t->unpack + (size_t)2 * t->ndev * t->nblk, h = 0;
-      TILED_HIP(hipMemcpy(&h, flag, sizeof(h), hipMemcpyDeviceToHost));
-      if (h) {
-        TILED_HIP(hipMemset(flag, 0, sizeof(h)));
-        return fail(BZR_ERR_CAPACITY, "bzr_tiled_trace: the frame had more survivors than the compact capacity " +
-                                          std::to_string(t->cap) + ": its outputs are incomplete (bzr_tiled_calibrate "
-                                          "or a larger cap)");
-      }
+    uint32_t *flag = t->unpack + (size_t)2 * t->ndev * t->nblk, h = 0;
+    TILED_HIP(hipMemcpy(&h, flag, sizeof(h), hipMemcpyDeviceToHost));
+    if (h) {
+      TILED_HIP(hipMemset(flag, 0, sizeof(h)));
+      return fail(BZR_ERR_CAPACITY, "bzr_tiled_trace: the frame had more survivors than the compact capacity " +
+                                        std::to_string(t->cap) + ": its outputs are incomplete (bzr_tiled_calibrate "
+                                        "or a larger cap)");
     }
   }
   return BZR_OK;
@@ -756,7 +771,7 @@ extern "C" bzr_status bzr_trace_tiled(bzr_ctx *const *ctxs, uint32_t nctx, const
   if (!rays || !out_rays || !out_status) return fail(BZR_ERR_INVALID_ARGUMENT, "bzr_trace_tiled: null buffer");
   bzr_tiled *t = nullptr;
   if (bzr_status s = bzr_tiled_create(ctxs, nctx, 1, n, tile_rays, BZR_GATHER_AUTO, &t)) return s;
-  bzr_status s = bzr_tiled_set_rays(t, rays, flags & BZR_DEVICE_PTRS);
+  bzr_status s = bzr_tiled_set_rays(t, rays, flags & (BZR_DEVICE_PTRS | BZR_RAYS_AOS));
   if (s == BZR_OK) s = bzr_tiled_trace(t, lenses, ri, nlens, out_rays, out_status, out_segments, flags);
   if (s == BZR_OK) s = bzr_tiled_sync(t);
   bzr_tiled_destroy(t);

@@ -2822,6 +2822,21 @@ struct Staging {  // carves device buffers out of a context-owned allocation
   }
 };
 
+// The caller's rays into the kernels' rows `r` ([6][n] on the device): copied from host memory and/or
+// transposed from [n][6] records (BZR_RAYS_AOS; a host source lands in `tmp` first).
+bzr_status rays_in(bzr_ctx *ctx, const float *rays, float *r, uint32_t n, bool host, bool aos, float *tmp) {
+  if (host) BZR_HIP(hipMemcpyAsync(aos ? tmp : r, rays, (size_t)n * 24, hipMemcpyHostToDevice, ctx->stream));
+  if (aos) BZR_HIP(bzr_rays_relayout(ctx->stream, host ? tmp : rays, r, n, true));
+  return BZR_OK;
+}
+// The kernels' output rows `d_out` to the caller's out_rays: transposed to [n][6] records (BZR_RAYS_AOS; for a
+// host destination into `tmp` first) and/or copied to host memory (queued, not waited for).
+bzr_status rays_out(bzr_ctx *ctx, const float *d_out, float *out_rays, uint32_t n, bool host, bool aos, float *tmp) {
+  if (aos) BZR_HIP(bzr_rays_relayout(ctx->stream, d_out, host ? tmp : out_rays, n, false));
+  if (host) BZR_HIP(hipMemcpyAsync(out_rays, aos ? tmp : d_out, (size_t)n * 24, hipMemcpyDeviceToHost, ctx->stream));
+  return BZR_OK;
+}
+
 bzr_status check_ctx_mesh(bzr_ctx *ctx, const bzr_mesh *mesh) {
   if (!ctx) return set_error(BZR_ERR_INVALID_ARGUMENT, "null context");
   if (!mesh) return set_error(BZR_ERR_INVALID_ARGUMENT, "null mesh");
@@ -2846,7 +2861,10 @@ bool use_staged(uint32_t flags, uint64_t n, uint64_t nb) {
 }
 // BZR_MODE_FAST runs on the culled pipeline's kernels only; the brute-force scan is the parity reference.
 constexpr uint32_t kKnownFlags = BZR_DEVICE_PTRS | BZR_MODE_FAST | BZR_ACCEL_NONE | BZR_PIPELINE_STAGED | BZR_PIPELINE_FUSED;
-bzr_status check_flags(uint32_t flags) {
+// aos_ok: the call takes BZR_RAYS_AOS (the ray-batch entries: intersect, refract, trace_chain)
+bzr_status check_flags(uint32_t flags, bool aos_ok = false) {
+  if ((flags & BZR_RAYS_AOS) && !aos_ok) return set_error(BZR_ERR_INVALID_ARGUMENT, "BZR_RAYS_AOS is not accepted by this call");
+  if (aos_ok) flags &= ~uint32_t(BZR_RAYS_AOS);
   if (flags & ~kKnownFlags) return set_error(BZR_ERR_INVALID_ARGUMENT, "unknown flag bits " + std::to_string(flags & ~kKnownFlags));
   if ((flags & BZR_PIPELINE_STAGED) && (flags & BZR_PIPELINE_FUSED))
     return set_error(BZR_ERR_INVALID_ARGUMENT, "BZR_PIPELINE_STAGED and BZR_PIPELINE_FUSED are exclusive");
@@ -3435,21 +3453,24 @@ extern "C" bzr_status bzr_mesh_size(const bzr_mesh *mesh, uint32_t *n) {
 
 extern "C" bzr_status bzr_intersect(bzr_ctx *ctx, const bzr_mesh *mesh, const float *rays, uint32_t n, float *hits,
                                     uint32_t flags) {
-  if (bzr_status s = check_flags(flags)) return s;
+  if (bzr_status s = check_flags(flags, true)) return s;
   if (bzr_status s = check_ctx_mesh(ctx, mesh)) return s;
   if (n == 0) return BZR_OK;
   if (!rays || !hits) return set_error(BZR_ERR_INVALID_ARGUMENT, "null buffer");
   DeviceGuard g(ctx->device);
   const float *d_rays = rays;
   float *d_hits = hits;
-  bool host = !(flags & BZR_DEVICE_PTRS);
-  if (host) {
+  const bool host = !(flags & BZR_DEVICE_PTRS), aos = (flags & BZR_RAYS_AOS) != 0;
+  if (host || aos) {
     size_t rb = (size_t)n * 6 * sizeof(float), hb = (size_t)n * 13 * sizeof(float);
-    if (bzr_status s = ensure_buffer(ctx->scratch, ctx->scratch_bytes, round256(rb) + round256(hb))) return s;
+    if (bzr_status s = ensure_buffer(ctx->scratch, ctx->scratch_bytes,
+                                     round256(rb) + (host ? round256(hb) : 0) + (host && aos ? round256(rb) : 0)))
+      return s;
     Staging st{static_cast<char *>(ctx->scratch)};
     float *r = st.take<float>((size_t)n * 6);
-    d_hits = st.take<float>((size_t)n * 13);
-    BZR_HIP(hipMemcpyAsync(r, rays, rb, hipMemcpyHostToDevice, ctx->stream));
+    if (host) d_hits = st.take<float>((size_t)n * 13);
+    float *tmp = host && aos ? st.take<float>((size_t)n * 6) : nullptr;
+    if (bzr_status s = rays_in(ctx, rays, r, n, host, aos, tmp)) return s;
     d_rays = r;
   }
   MeshView mv = view_of(mesh);
@@ -3519,7 +3540,7 @@ extern "C" bzr_status bzr_patch_intersect(bzr_ctx *ctx, const bzr_mesh *mesh, co
 extern "C" bzr_status bzr_refract(bzr_ctx *ctx, const bzr_mesh *mesh, float ri, const float *rays, const uint32_t *expected,
                                   uint32_t expected_all, uint32_t n, float *out_rays, uint32_t *out_status,
                                   uint32_t flags) {
-  if (bzr_status s = check_flags(flags)) return s;
+  if (bzr_status s = check_flags(flags, true)) return s;
   if (bzr_status s = check_ctx_mesh(ctx, mesh)) return s;
   if (n == 0) return BZR_OK;
   if (!rays || !out_rays || !out_status) return set_error(BZR_ERR_INVALID_ARGUMENT, "null buffer");
@@ -3528,19 +3549,25 @@ extern "C" bzr_status bzr_refract(bzr_ctx *ctx, const bzr_mesh *mesh, float ri, 
   const uint32_t *d_exp = expected;
   float *d_out = out_rays;
   uint32_t *d_st = out_status;
-  bool host = !(flags & BZR_DEVICE_PTRS);
-  if (host) {
+  const bool host = !(flags & BZR_DEVICE_PTRS), aos = (flags & BZR_RAYS_AOS) != 0;
+  float *tmp = nullptr;  // host + AoS: the records on the device, in and out
+  if (host || aos) {
     size_t rb = (size_t)n * 24, ib = (size_t)n * 4;
-    if (bzr_status s = ensure_buffer(ctx->scratch, ctx->scratch_bytes, 2 * round256(rb) + 2 * round256(ib))) return s;
+    if (bzr_status s = ensure_buffer(ctx->scratch, ctx->scratch_bytes,
+                                     2 * round256(rb) + (host ? 2 * round256(ib) : 0) + (host && aos ? round256(rb) : 0)))
+      return s;
     Staging st{static_cast<char *>(ctx->scratch)};
     float *r = st.take<float>((size_t)n * 6);
-    uint32_t *e = st.take<uint32_t>(n);
     d_out = st.take<float>((size_t)n * 6);
-    d_st = st.take<uint32_t>(n);
-    BZR_HIP(hipMemcpyAsync(r, rays, rb, hipMemcpyHostToDevice, ctx->stream));
-    if (expected) BZR_HIP(hipMemcpyAsync(e, expected, ib, hipMemcpyHostToDevice, ctx->stream));
+    if (host) {
+      uint32_t *e = st.take<uint32_t>(n);
+      d_st = st.take<uint32_t>(n);
+      if (expected) BZR_HIP(hipMemcpyAsync(e, expected, ib, hipMemcpyHostToDevice, ctx->stream));
+      d_exp = expected ? e : nullptr;
+    }
+    if (host && aos) tmp = st.take<float>((size_t)n * 6);
+    if (bzr_status s = rays_in(ctx, rays, r, n, host, aos, tmp)) return s;
     d_rays = r;
-    d_exp = expected ? e : nullptr;
   }
   MeshView mv = view_of(mesh, ri);
   if (use_scan(flags)) {
@@ -3570,8 +3597,8 @@ extern "C" bzr_status bzr_refract(bzr_ctx *ctx, const bzr_mesh *mesh, float ri, 
         return s;
   }
   BZR_HIP(hipGetLastError());
+  if (bzr_status s = rays_out(ctx, d_out, out_rays, n, host, aos, tmp)) return s;
   if (host) {
-    BZR_HIP(hipMemcpyAsync(out_rays, d_out, (size_t)n * 24, hipMemcpyDeviceToHost, ctx->stream));
     BZR_HIP(hipMemcpyAsync(out_status, d_st, (size_t)n * 4, hipMemcpyDeviceToHost, ctx->stream));
     BZR_HIP(hipStreamSynchronize(ctx->stream));
   }
@@ -3581,7 +3608,7 @@ extern "C" bzr_status bzr_refract(bzr_ctx *ctx, const bzr_mesh *mesh, float ri, 
 extern "C" bzr_status bzr_trace_chain(bzr_ctx *ctx, const bzr_mesh *const *lenses, const float *ri, uint32_t nlens,
                                       const float *rays, uint32_t n, float *out_rays, uint32_t *out_status,
                                       uint32_t *out_segments, uint32_t flags) {
-  if (bzr_status s = check_flags(flags)) return s;
+  if (bzr_status s = check_flags(flags, true)) return s;
   if (!ctx) return set_error(BZR_ERR_INVALID_ARGUMENT, "null context");
   if (nlens == 0 || nlens > kMaxLenses) return set_error(BZR_ERR_INVALID_ARGUMENT, "nlens must be 1..8");
   if (!lenses || !ri) return set_error(BZR_ERR_INVALID_ARGUMENT, "null lens list");
@@ -3598,16 +3625,22 @@ extern "C" bzr_status bzr_trace_chain(bzr_ctx *ctx, const bzr_mesh *const *lense
   const float *d_rays = rays;
   float *d_out = out_rays;
   uint32_t *d_st = out_status, *d_seg = out_segments;
-  bool host = !(flags & BZR_DEVICE_PTRS);
-  if (host) {
+  const bool host = !(flags & BZR_DEVICE_PTRS), aos = (flags & BZR_RAYS_AOS) != 0;
+  float *tmp = nullptr;  // host + AoS: the records on the device, in and out
+  if (host || aos) {
     size_t rb = (size_t)n * 24, ib = (size_t)n * 4;
-    if (bzr_status s = ensure_buffer(ctx->scratch, ctx->scratch_bytes, 2 * round256(rb) + 2 * round256(ib))) return s;
+    if (bzr_status s = ensure_buffer(ctx->scratch, ctx->scratch_bytes,
+                                     2 * round256(rb) + (host ? 2 * round256(ib) : 0) + (host && aos ? round256(rb) : 0)))
+      return s;
     Staging st{static_cast<char *>(ctx->scratch)};
     float *r = st.take<float>((size_t)n * 6);
     d_out = st.take<float>((size_t)n * 6);
-    d_st = st.take<uint32_t>(n);
-    d_seg = st.take<uint32_t>(n);
-    BZR_HIP(hipMemcpyAsync(r, rays, rb, hipMemcpyHostToDevice, ctx->stream));
+    if (host) {
+      d_st = st.take<uint32_t>(n);
+      d_seg = st.take<uint32_t>(n);
+    }
+    if (host && aos) tmp = st.take<float>((size_t)n * 6);
+    if (bzr_status s = rays_in(ctx, rays, r, n, host, aos, tmp)) return s;
     d_rays = r;
   }
   if (use_scan(flags)) {
@@ -3649,8 +3682,8 @@ extern "C" bzr_status bzr_trace_chain(bzr_ctx *ctx, const bzr_mesh *const *lense
     }
     BZR_HIP(hipGetLastError());
   }
+  if (bzr_status s = rays_out(ctx, d_out, out_rays, n, host, aos, tmp)) return s;
   if (host) {
-    BZR_HIP(hipMemcpyAsync(out_rays, d_out, (size_t)n * 24, hipMemcpyDeviceToHost, ctx->stream));
     BZR_HIP(hipMemcpyAsync(out_status, d_st, (size_t)n * 4, hipMemcpyDeviceToHost, ctx->stream));
     if (out_segments)
       BZR_HIP(hipMemcpyAsync(out_segments, d_seg, (size_t)n * 4, hipMemcpyDeviceToHost, ctx->stream));

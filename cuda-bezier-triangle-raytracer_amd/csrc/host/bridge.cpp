@@ -10,6 +10,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <type_traits>
 
 #include "bzr/bzr.hpp"
 #include "single_ray.hpp"
@@ -49,24 +50,15 @@ struct DeviceMesh {
 };
 
 namespace {
-std::vector<float> raysToSoa(Ray const *rays, std::size_t n) {
-  std::vector<float> soa(6 * n);
-  for (std::size_t i = 0; i < n; ++i) {
-    for (int k = 0; k < 3; ++k) {
-      soa[k * n + i] = rays[i].mStart(k);
-      soa[(3 + k) * n + i] = rays[i].mDirection(k);
-    }
-  }
-  return soa;
-}
-Ray soaToRay(std::vector<float> const &soa, std::size_t n, std::size_t i) {
-  Ray r;
-  for (int k = 0; k < 3; ++k) {
-    r.mStart(k) = soa[k * n + i];
-    r.mDirection(k) = soa[(3 + k) * n + i];
-  }
-  return r;
-}
+// The batch calls hand the caller's Ray arrays to the C ABI as they are (BZR_RAYS_AOS: [n][6] records, transposed
+// on the device) and RefractionResult arrays as uint32 words.
+static_assert(sizeof(Ray) == 6 * sizeof(float) && alignof(Ray) == alignof(float) && std::is_standard_layout<Ray>::value,
+              "Ray must be the 24-byte [start xyz, direction xyz] record BZR_RAYS_AOS reads");
+static_assert(sizeof(RefractionResult) == sizeof(uint32_t), "RefractionResult must be a uint32 word");
+float const *records(Ray const *r) { return reinterpret_cast<float const *>(r); }
+float *records(Ray *r) { return reinterpret_cast<float *>(r); }
+uint32_t *words(RefractionResult *s) { return reinterpret_cast<uint32_t *>(s); }
+uint32_t const *words(RefractionResult const *s) { return reinterpret_cast<uint32_t const *>(s); }
 BezierIntersection hitFromSoa(std::vector<float> const &h, std::size_t n, std::size_t i) {
   BezierIntersection b;
   b.mIntersection.mDistance = h[i];
@@ -93,15 +85,9 @@ void traceChain(std::vector<BezierLens const *> const &lenses, Ray const *rays, 
   }
   for (std::size_t off = 0; off < n; off += kMaxBatch) {
     const std::size_t m = std::min(kMaxBatch, n - off);
-    std::vector<float> in = raysToSoa(rays + off, m), out(6 * m);
-    std::vector<uint32_t> st(m);
-    check(bzr_trace_chain(c.get(), meshes.data(), ri.data(), static_cast<uint32_t>(meshes.size()), in.data(),
-                          static_cast<uint32_t>(m), out.data(), st.data(), outSegments ? outSegments + off : nullptr,
-                          BZR_HOST_PTRS));
-    for (std::size_t i = 0; i < m; ++i) {
-      outRays[off + i] = soaToRay(out, m, i);
-      outStatus[off + i] = static_cast<RefractionResult>(st[i]);
-    }
+    check(bzr_trace_chain(c.get(), meshes.data(), ri.data(), static_cast<uint32_t>(meshes.size()), records(rays + off),
+                          static_cast<uint32_t>(m), records(outRays + off), words(outStatus + off),
+                          outSegments ? outSegments + off : nullptr, BZR_HOST_PTRS | BZR_RAYS_AOS));
   }
 }
 
@@ -117,15 +103,9 @@ void traceChainTiled(std::vector<Context *> const &ctxs, std::vector<BezierLens 
     for (auto const *l : lenses) meshes.push_back(l->getMesh().device(*c));
   }
   if (n > UINT32_MAX) throw std::length_error("traceChainTiled: more than 2^32-1 rays in one call");
-  std::vector<float> in = raysToSoa(rays, n), out(6 * n);
-  std::vector<uint32_t> st(n);
   check(bzr_trace_tiled(handles.data(), static_cast<uint32_t>(handles.size()), meshes.data(), ri.data(),
-                        static_cast<uint32_t>(lenses.size()), in.data(), static_cast<uint32_t>(n), tileRays, out.data(),
-                        st.data(), outSegments, BZR_HOST_PTRS));
-  for (std::size_t i = 0; i < n; ++i) {
-    outRays[i] = soaToRay(out, n, i);
-    outStatus[i] = static_cast<RefractionResult>(st[i]);
-  }
+                        static_cast<uint32_t>(lenses.size()), records(rays), static_cast<uint32_t>(n), tileRays,
+                        records(outRays), words(outStatus), outSegments, BZR_HOST_PTRS | BZR_RAYS_AOS));
 }
 
 TiledChain::TiledChain(std::vector<std::vector<Context *>> const &slots, std::vector<BezierLens const *> const &lenses,
@@ -155,8 +135,7 @@ int TiledChain::transport() const {
 }
 
 void TiledChain::setRays(Ray const *rays) {
-  std::vector<float> soa = raysToSoa(rays, mN);
-  check(bzr_tiled_set_rays(mPlan, soa.data(), BZR_HOST_PTRS));
+  check(bzr_tiled_set_rays(mPlan, records(rays), BZR_HOST_PTRS | BZR_RAYS_AOS));
 }
 
 void TiledChain::setRaysDevice(float const *raysSoaOnDevice0) {
@@ -169,14 +148,8 @@ void TiledChain::trace(float *outRays, uint32_t *outStatus, uint32_t *outSegment
 }
 
 void TiledChain::trace(Ray *outRays, RefractionResult *outStatus, uint32_t *outSegments, uint32_t flags) {
-  std::vector<float> out(6 * mN);
-  std::vector<uint32_t> st(mN);
-  check(bzr_tiled_trace(mPlan, mMeshes.data(), mRi.data(), static_cast<uint32_t>(mRi.size()), out.data(), st.data(),
-                        outSegments, flags & ~uint32_t(BZR_DEVICE_PTRS)));
-  for (std::size_t i = 0; i < mN; ++i) {
-    outRays[i] = soaToRay(out, mN, i);
-    outStatus[i] = static_cast<RefractionResult>(st[i]);
-  }
+  check(bzr_tiled_trace(mPlan, mMeshes.data(), mRi.data(), static_cast<uint32_t>(mRi.size()), records(outRays),
+                        words(outStatus), outSegments, (flags & ~uint32_t(BZR_DEVICE_PTRS)) | BZR_RAYS_AOS));
 }
 
 uint32_t TiledChain::calibrate(uint32_t flags) {
@@ -207,8 +180,9 @@ void BezierMesh::intersect(Ray const *rays, std::size_t n, BezierIntersection *o
   bzr_mesh *dm = device(c);
   for (std::size_t off = 0; off < n; off += bzr::kMaxBatch) {
     const std::size_t m = std::min(bzr::kMaxBatch, n - off);
-    std::vector<float> in = bzr::raysToSoa(rays + off, m), hits(13 * m);
-    bzr::check(bzr_intersect(c.get(), dm, in.data(), static_cast<uint32_t>(m), hits.data(), BZR_HOST_PTRS));
+    std::vector<float> hits(13 * m);
+    bzr::check(bzr_intersect(c.get(), dm, bzr::records(rays + off), static_cast<uint32_t>(m), hits.data(),
+                             BZR_HOST_PTRS | BZR_RAYS_AOS));
     for (std::size_t i = 0; i < m; ++i) {
       out[off + i] = bzr::hitFromSoa(hits, m, i);
       if (patchIndex) std::memcpy(&patchIndex[off + i], &hits[12 * m + i], 4);
@@ -234,15 +208,9 @@ void BezierLens::refract(Ray const *rays, RefractionResult const *expected, std:
   bzr_mesh *dm = mMesh.device(c);
   for (std::size_t off = 0; off < n; off += bzr::kMaxBatch) {
     const std::size_t m = std::min(bzr::kMaxBatch, n - off);
-    std::vector<float> in = bzr::raysToSoa(rays + off, m), out(6 * m);
-    std::vector<uint32_t> exp(m), st(m);
-    for (std::size_t i = 0; i < m; ++i) exp[i] = static_cast<uint32_t>(expected[off + i]);
-    bzr::check(bzr_refract(c.get(), dm, mRefractiveIndex, in.data(), exp.data(), 0u, static_cast<uint32_t>(m),
-                           out.data(), st.data(), BZR_HOST_PTRS));
-    for (std::size_t i = 0; i < m; ++i) {
-      outRays[off + i] = bzr::soaToRay(out, m, i);
-      outStatus[off + i] = static_cast<RefractionResult>(st[i]);
-    }
+    bzr::check(bzr_refract(c.get(), dm, mRefractiveIndex, bzr::records(rays + off), bzr::words(expected + off), 0u,
+                           static_cast<uint32_t>(m), bzr::records(outRays + off), bzr::words(outStatus + off),
+                           BZR_HOST_PTRS | BZR_RAYS_AOS));
   }
 }
 

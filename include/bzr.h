@@ -91,7 +91,14 @@ enum {
    * 0.62 -> 0.40 ms), and lone cfg2 frames now run as fast fused as staged (0.395 vs 0.392 ms, 341 rays per
    * patch).  The first call of a size, or calls of changing sizes, run in input order. */
   BZR_PIPELINE_STAGED = 8u,
-  BZR_PIPELINE_FUSED = 16u
+  BZR_PIPELINE_FUSED = 16u,
+  /* Ray records in the reference's layout: rays / out_rays are [n][6] (per ray start xyz, direction xyz --
+   * `Ray` of reference/3dGeomUtil.h:168, 24 bytes) instead of [6][n].  Host or device pointers alike; the library
+   * transposes on the device (48 bytes per ray each way, HBM-bound), so a C++ caller hands its std::vector<Ray>
+   * over with no host-side conversion.  Accepted by bzr_intersect (rays), bzr_refract, bzr_trace_chain,
+   * bzr_trace_tiled, bzr_tiled_set_rays (rays) and bzr_tiled_trace (out_rays); other calls reject it.  Other
+   * arrays (hits, status, segments, expected) keep their layouts. */
+  BZR_RAYS_AOS = 32u
 };
 
 enum { BZR_WHAT_FOLLOW0 = 0, BZR_WHAT_FOLLOW1 = 1, BZR_WHAT_FOLLOW2 = 2, BZR_WHAT_NONE = 3, BZR_WHAT_INTERSECT = 4 };
@@ -244,7 +251,7 @@ bzr_status bzr_tiled_info(const bzr_tiled *plan, int32_t *transport, uint32_t *s
  * each device's share and sends it there (one peer copy per other device, (ndev - 1) / ndev of the frame
  * in all), queued on ctxs[0]'s stream and ordered before the next bzr_tiled_trace without a host wait.
  * With one device the frame is the share: one copy, nothing extracted.  The rays stay resident for every
- * following frame. */
+ * following frame.  BZR_RAYS_AOS: the rays are [n][6] records, transposed on device 0 after the copy. */
 bzr_status bzr_tiled_set_rays(bzr_tiled *plan, const float *rays_soa, uint32_t flags);
 /* Device d's share input [6][share_rays[d]] (device memory on device d), for callers that generate rays
  * on the devices: write it (ordered before the next bzr_tiled_trace, e.g. then bzr_tiled_sync). */
@@ -256,7 +263,8 @@ bzr_status bzr_tiled_share_rays(bzr_tiled *plan, uint32_t device_index, float **
  * device; the call returns once the frame is queued (no host wait), frames on different slots overlap,
  * and the outputs are ready on bzr_tiled_stream's stream (or after bzr_tiled_sync) -- keep one set of
  * outputs per frame in flight.  Host pointers: synchronous, and a compact frame with more survivors than
- * the capacity returns BZR_ERR_CAPACITY at once.  Mode / pipeline flags pass through. */
+ * the capacity returns BZR_ERR_CAPACITY at once.  Mode / pipeline flags pass through.  BZR_RAYS_AOS: out_rays
+ * as [n][6] records (device 0 transposes the frame's rays on the stream that produced them, 48 B per ray). */
 bzr_status bzr_tiled_trace(bzr_tiled *plan, const bzr_mesh *const *lenses, const float *refractive_index,
                            uint32_t nlens, float *out_rays_soa, uint32_t *out_status, uint32_t *out_segments,
                            uint32_t flags);

@@ -71,9 +71,19 @@ def test_flags_are_validated_first(bzr):
         assert msg in L.bzr_last_error()
     # every documented combination passes the flag check (and then fails on the null context)
     for flags in (0, bzr.DEVICE_PTRS, bzr.MODE_FAST, bzr.ACCEL_NONE, bzr.PIPELINE_STAGED, bzr.PIPELINE_FUSED,
-                  bzr.DEVICE_PTRS | bzr.MODE_FAST | bzr.PIPELINE_FUSED):
+                  bzr.DEVICE_PTRS | bzr.MODE_FAST | bzr.PIPELINE_FUSED, bzr.RAYS_AOS, bzr.RAYS_AOS | bzr.DEVICE_PTRS):
         assert L.bzr_intersect(None, None, None, 0, None, flags) == 1
         assert b"null context" in L.bzr_last_error()
+    # the ray-record layout: taken by the ray-batch calls, refused by the others
+    assert L.bzr_trace_chain(None, None, f, 1, None, 0, None, None, None, bzr.RAYS_AOS) == 1
+    assert b"null context" in L.bzr_last_error()
+    assert L.bzr_refract(None, None, ctypes.c_float(1.3), None, None, 0, 0, None, None, bzr.RAYS_AOS) == 1
+    assert b"null context" in L.bzr_last_error()
+    assert L.bzr_patch_intersect(None, None, None, None, None, 0, None, bzr.RAYS_AOS) == 1
+    assert b"BZR_RAYS_AOS" in L.bzr_last_error()
+    # and the Python helpers check the [n, 6] shape before any call
+    with pytest.raises(bzr.BzrError, match=r"\[n, 6\]"):
+        bzr.intersect(None, None, np.zeros((6, 10), np.float32), mode=bzr.RAYS_AOS)
 
 
 def test_trace_tiled_validates_before_touching_a_device(bzr):

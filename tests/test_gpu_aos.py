@@ -1,0 +1,112 @@
+"""BZR_RAYS_AOS: the ray-batch calls taking the reference's Ray records ([n][6]: start xyz, direction xyz;
+reference/3dGeomUtil.h:168) instead of [6][n] rows, transposed on the device.  The bar is bit-identity with the
+same call on rows (which tests/test_gpu_parity.py pins to the oracle), for host and device pointers, both
+culled pipelines, the brute-force scan, ragged sizes (not a multiple of the 256-ray transpose block) and the
+multi-frame plan with frames in flight.
+"""
+import numpy as np
+import pytest
+
+from bzr_amd.configs import CONFIGS, build_lens, grid_rays
+
+pytestmark = pytest.mark.gpu
+
+
+def _u32(x):
+    x = x.cpu().numpy() if hasattr(x, "cpu") else np.asarray(x)
+    return np.ascontiguousarray(x).view(np.uint32)
+
+
+def _cfg4(bzr, ctx):
+    cfg = CONFIGS["cfg4"]
+    patches = [build_lens(bzr.TriMesh, lens).bezier_patches() for lens in cfg.lenses]
+    return cfg, patches, [lens.ri for lens in cfg.lenses], [bzr.DeviceMesh(ctx, p) for p in patches]
+
+
+@pytest.mark.parametrize("pipeline", ["fused", "staged", "scan"])
+@pytest.mark.parametrize("device", [False, True])
+def test_trace_chain_records_equal_rows(bzr, ctx, pipeline, device):
+    import torch
+
+    cfg, _, ri, lenses = _cfg4(bzr, ctx)
+    rays = grid_rays(cfg, side=128)[:, :16001].copy()  # ragged: 62.5 transpose blocks
+    mode = {"fused": bzr.PIPELINE_FUSED, "staged": bzr.PIPELINE_STAGED, "scan": bzr.ACCEL_NONE}[pipeline]
+    want = bzr.trace_chain(ctx, lenses, ri, rays, mode=mode)
+    rec = np.ascontiguousarray(rays.T)
+    if device:
+        rec = torch.from_numpy(rec).cuda()
+    got = bzr.trace_chain(ctx, lenses, ri, rec, mode=mode | bzr.RAYS_AOS)
+    if device:
+        torch.cuda.synchronize()
+    assert tuple(got[0].shape) == (rays.shape[1], 6)
+    assert np.array_equal(_u32(got[0]), _u32(want[0]).T)
+    assert np.array_equal(_u32(got[1]), _u32(want[1]))
+    assert np.array_equal(_u32(got[2]), _u32(want[2]))
+    assert int(np.asarray(want[2]).sum()) > rays.shape[1]
+
+
+@pytest.mark.parametrize("device", [False, True])
+def test_refract_and_intersect_records_equal_rows(bzr, ctx, device):
+    import torch
+
+    cfg, _, ri, lenses = _cfg4(bzr, ctx)
+    rays = grid_rays(cfg, side=128)[:, :9999].copy()
+    rng = np.random.default_rng(3)
+    expected = rng.integers(1, 3, rays.shape[1]).astype(np.uint32)  # per-ray INSIDE / OUTSIDE
+    rec = np.ascontiguousarray(rays.T)
+    dev = (lambda a: torch.from_numpy(a).cuda()) if device else (lambda a: a)
+    want_h = bzr.intersect(ctx, lenses[0], rays)
+    got_h = bzr.intersect(ctx, lenses[0], dev(rec), mode=bzr.RAYS_AOS)
+    want_r = bzr.refract(ctx, lenses[0], ri[0], rays, expected=expected)
+    got_r = bzr.refract(ctx, lenses[0], ri[0], dev(rec), expected=dev(expected.view(np.int32)), mode=bzr.RAYS_AOS)
+    if device:
+        torch.cuda.synchronize()
+    assert np.array_equal(_u32(got_h), _u32(want_h))  # hits keep their [13, n] rows
+    assert np.array_equal(_u32(got_r[0]), _u32(want_r[0]).T)
+    assert np.array_equal(_u32(got_r[1]), _u32(want_r[1]))
+
+
+def test_trace_tiled_records_equal_rows(bzr, ctx):
+    cfg, patches, ri, single = _cfg4(bzr, ctx)
+    rays = grid_rays(cfg, side=256)[:, :60000].copy()
+    want = bzr.trace_chain(ctx, single, ri, rays)
+    for nctx in (1, 2):
+        ctxs = [bzr.Context(0) for _ in range(nctx)]
+        lenses = [[bzr.DeviceMesh(c, p) for p in patches] for c in ctxs]
+        got = bzr.trace_tiled(ctxs, lenses, ri, np.ascontiguousarray(rays.T), tile_rays=4096, mode=bzr.RAYS_AOS)
+        assert np.array_equal(_u32(got[0]), _u32(want[0]).T)
+        assert np.array_equal(_u32(got[1]), _u32(want[1])) and np.array_equal(_u32(got[2]), _u32(want[2]))
+
+
+@pytest.mark.parametrize("transport,ndev", [("direct", 1), ("peer", 2)])
+@pytest.mark.parametrize("host", [False, True])
+def test_tiled_plan_records_frames_in_flight(bzr, ctx, transport, ndev, host):
+    """Record rays into the plan, record outputs from it: 2 slots, 4 frames queued back to back with a
+    different refractive index each (device outputs) or synchronous host frames; each equals one
+    bzr_trace_chain on rows -- a slot's row staging reused before its transposition would fail."""
+    import torch
+
+    cfg, patches, _, _ = _cfg4(bzr, ctx)
+    rays = grid_rays(cfg, side=256)
+    n = rays.shape[1]
+    tp = {"direct": bzr.GATHER_DIRECT, "peer": bzr.GATHER_PEER}[transport]
+    slots = [[bzr.Context(0) for _ in range(ndev)] for _ in range(2)]
+    lenses = [[bzr.DeviceMesh(c, p) for p in patches] for c in slots[0]]
+    plan = bzr.TiledPlan(slots, n, tile_rays=4096, transport=tp)
+    rec = np.ascontiguousarray(rays.T)
+    plan.set_rays(rec if host else torch.from_numpy(rec).cuda(), mode=bzr.RAYS_AOS)
+    ris = [1.3, 1.45, 1.2, 1.6]
+    if host:
+        outs = [(np.empty((n, 6), np.float32), np.empty(n, np.uint32), np.empty(n, np.uint32)) for _ in ris]
+    else:
+        outs = [(torch.empty((n, 6), device="cuda"), torch.empty(n, dtype=torch.int32, device="cuda"),
+                 torch.empty(n, dtype=torch.int32, device="cuda")) for _ in ris]
+    for r, o in zip(ris, outs):
+        plan.trace(lenses, [r, r], *o, mode=bzr.RAYS_AOS)
+    plan.sync()
+    single = [bzr.DeviceMesh(ctx, p) for p in patches]
+    for r, o in zip(ris, outs):
+        w = bzr.trace_chain(ctx, single, [r, r], rays)
+        assert np.array_equal(_u32(o[0]), _u32(w[0]).T)
+        assert np.array_equal(_u32(o[1]), _u32(w[1])) and np.array_equal(_u32(o[2]), _u32(w[2]))
+    plan.close()
