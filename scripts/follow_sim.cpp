@@ -1,0 +1,66 @@
+// How many of the staged path's follow-side retries (reference/bezierMesh.cpp:213-218: a patch whose Newton
+// point left it across side k retries neighbour k with LimitPlaneIntersection::cNone) go to a neighbour that
+// passed its OWN planar gate for the same ray.  The limit only drops the gate's barycentric range test
+// (reference/bezierTriangle.cpp:124-131); everything after it is the same arithmetic, so such a retry
+// recomputes the neighbour's own pair bit for bit -- a result the mesh loop already has.  Host only: the
+// product's arithmetic (single_ray.cpp) with a probe telling whether the Newton stage ran (= the gate passed).
+// usage: follow_sim cfg5|cfg3|cfg4 [rays]
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <random>
+#include <string>
+#include <vector>
+
+static int g_ran = 0;
+#define BZR_NEWTON_PROBE(i, m, d) (g_ran = 1)
+#include "../cuda-bezier-triangle-raytracer_amd/csrc/host/single_ray.cpp"
+
+#include "bzr/bzr.hpp"
+
+int main(int argc, char **argv) {
+  const std::string cfg = argc > 1 ? argv[1] : "cfg5";
+  const int nrays = argc > 2 ? std::atoi(argv[2]) : 1000;
+  Mesh m;
+  float x0 = 0.0f, ylo = -4.2f, yhi = 4.2f, zlo = -2.1f, zhi = 2.1f;
+  if (cfg == "cfg3") {
+    m.readMesh("cuda-bezier-triangle-raytracer_amd/bzr_amd/data/robot.stl");
+    m.splitTriangles(int32_t(8));
+    x0 = -100.0f; ylo = zlo = -25.0f; yhi = zhi = 25.0f;
+  } else {
+    const int sec = cfg == "cfg5" ? 224 : 32, belts = cfg == "cfg5" ? 224 : 16;
+    m.makeEllipsoid(sec, belts, Vector(1.0f, 4.0f, 2.0f));
+    m += Vector{10.0f, 0.0f, 0.0f};
+  }
+  m.standardizeVertices();
+  m.standardizeNormals();
+  BezierMesh mesh(m);
+  std::mt19937 rng(11);
+  std::uniform_real_distribution<float> uy(ylo, yhi), uz(zlo, zhi);
+  long pairs = 0, follows = 0, nbr_gated = 0, nbr_gated_intersect = 0, mismatch = 0;
+  for (int r = 0; r < nrays; ++r) {
+    Ray ray(Vertex{x0, uy(rng), uz(rng)}, Vector{1.0f, 0.0f, 0.0f});
+    for (uint32_t b = 0; b < mesh.size(); ++b) {
+      g_ran = 0;
+      BezierIntersection c = bzr::host::patchIntersect(mesh[b], ray, false);
+      if (!g_ran) continue;
+      ++pairs;
+      const uint32_t w = static_cast<uint32_t>(c.mWhat);
+      if (w > 2u) continue;
+      ++follows;
+      const uint32_t nbr = mesh[b].getNeighbours()[w];
+      g_ran = 0;
+      BezierIntersection own = bzr::host::patchIntersect(mesh[nbr], ray, false);  // the neighbour's own pair
+      if (!g_ran) continue;
+      ++nbr_gated;
+      BezierIntersection retry = bzr::host::patchIntersect(mesh[nbr], ray, true);  // what the mesh loop runs
+      if (std::memcmp(&own, &retry, sizeof own) != 0) ++mismatch;
+      if (own.mWhat == BezierIntersection::What::cIntersect) ++nbr_gated_intersect;
+    }
+  }
+  std::printf("{\"config\": \"%s\", \"rays\": %d, \"pairs\": %ld, \"follows\": %ld, \"follows_to_gated_neighbour\": %ld, "
+              "\"of_which_neighbour_intersects\": %ld, \"retry_differs_from_own_pair\": %ld, \"skippable_frac\": %.4f}\n",
+              cfg.c_str(), nrays, pairs, follows, nbr_gated, nbr_gated_intersect, mismatch,
+              follows ? (double)nbr_gated / follows : 0.0);
+  return 0;
+}
