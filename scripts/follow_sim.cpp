@@ -54,7 +54,16 @@ int main(int argc, char **argv) {
       if (!g_ran) continue;
       ++nbr_gated;
       BezierIntersection retry = bzr::host::patchIntersect(mesh[nbr], ray, true);  // what the mesh loop runs
-      if (std::memcmp(&own, &retry, sizeof own) != 0) ++mismatch;
+      auto bits = [](BezierIntersection const &h) {  // every field (the struct has padding after mValid)
+        float f[12] = {h.mIntersection.mPoint(0), h.mIntersection.mPoint(1), h.mIntersection.mPoint(2),
+                       h.mIntersection.mCosIncidence, h.mIntersection.mDistance, h.mBarycentric(0), h.mBarycentric(1),
+                       h.mBarycentric(2), h.mNormal(0), h.mNormal(1), h.mNormal(2), static_cast<float>(h.mWhat)};
+        std::vector<uint32_t> w(12);
+        std::memcpy(w.data(), f, sizeof f);
+        w.push_back(h.mIntersection.mValid);
+        return w;
+      };
+      if (bits(own) != bits(retry)) ++mismatch;
       if (own.mWhat == BezierIntersection::What::cIntersect) ++nbr_gated_intersect;
     }
   }
