@@ -72,6 +72,7 @@ _SIGS = {
     "bzr_mesh_destroy": [_P],
     "bzr_mesh_size": [_P, ctypes.POINTER(_U32)],
     "bzr_intersect": [_P, _P, _P, _U32, _P, _U32],
+    "bzr_intersect_records": [_P, _P, _P, _U32, _P, _P, _U32],
     "bzr_patch_intersect": [_P, _P, _P, _P, _P, _U32, _P, _U32],
     "bzr_refract": [_P, _P, _F, _P, _P, _U32, _U32, _P, _P, _U32],
     "bzr_trace_chain": [_P, _P, _P, _U32, _P, _U32, _P, _P, _P, _U32],
@@ -336,6 +337,27 @@ def intersect(ctx: Context, mesh: DeviceMesh, rays, out=None, mode=MODE_PARITY):
     with _stream_for(ctx, res):
         _check(lib().bzr_intersect(ctx.handle, mesh.handle, r.ptr, n, o.ptr, res | mode))
     return out
+
+
+HIT_RECORD_WORDS = 13  # bzr_hit_record: valid, point xyz, cos, distance, bary xyz, normal xyz, what
+
+
+def intersect_records(ctx: Context, mesh: DeviceMesh, rays, records=None, patch=None, mode=MODE_PARITY):
+    """bzr_intersect_records: the hits as the reference's BezierIntersection records -> (records uint32 [n, 13]
+    (view float words with .view(float32)), patch [n]).  Same values as intersect()'s rows."""
+    n = _n_of(rays, mode)
+    if records is None and _is_tensor(rays):
+        import torch
+
+        records = torch.empty((n, HIT_RECORD_WORDS), dtype=torch.int32, device=rays.device)
+    elif records is None:
+        records = np.empty((n, HIT_RECORD_WORDS), np.uint32)
+    patch = _empty_like(rays, 0, np.uint32, mode) if patch is None else patch
+    r, o, p_ = _Buf(rays, np.float32), _Buf(records, np.uint32, True), _Buf(patch, np.uint32, True)
+    res = _residency(r, o, p_)
+    with _stream_for(ctx, res):
+        _check(lib().bzr_intersect_records(ctx.handle, mesh.handle, r.ptr, n, o.ptr, p_.ptr, res | mode))
+    return records, patch
 
 
 def patch_intersect(ctx: Context, mesh: DeviceMesh, patch_index, limit, rays, out=None):

@@ -50,3 +50,6 @@ struct bzr_ctx {
 // BZR_RAYS_AOS (frame_pack.hip): n rays between the reference's [n][6] records and the kernels' [6][n] rows,
 // device to device on `stream` (to_soa: src AoS -> dst rows; else rows -> AoS).  src and dst must not overlap.
 hipError_t bzr_rays_relayout(hipStream_t stream, const float *src, float *dst, uint32_t n, bool to_soa);
+// bzr_intersect_records (frame_pack.hip): hit rows [13][n] on the device -> n bzr_hit_record at `records` and the
+// patch words at `patch` (may be null), on `stream`.
+hipError_t bzr_hits_to_records(hipStream_t stream, const float *rows, uint32_t n, void *records, uint32_t *patch);

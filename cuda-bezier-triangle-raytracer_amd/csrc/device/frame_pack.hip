@@ -171,12 +171,49 @@ __global__ __launch_bounds__(kPackThreads) void k_rays_soa_to_aos(const float *_
   }
 }
 
+// bzr_intersect_records: hit rows ([13][n]: t, point, cos, bary, normal, what, patch) -> n bzr_hit_record (the
+// reference's BezierIntersection, 13 words) + the patch words.  256 hits' 13 KB through LDS per block, the
+// records written as one contiguous run of 13 x 256 words.
+constexpr uint32_t kHitWords = 13;
+__global__ __launch_bounds__(kPackThreads) void k_hits_to_records(const float *__restrict__ rows, uint32_t n,
+                                                                  uint32_t *__restrict__ rec,
+                                                                  uint32_t *__restrict__ patch) {
+  __shared__ uint32_t t[kHitWords * kPackThreads];
+  const size_t r0 = (size_t)blockIdx.x * kPackThreads;
+  const uint32_t m = static_cast<uint32_t>(min<size_t>(kPackThreads, n - r0)), i = threadIdx.x;
+  if (i < m) {
+    const size_t g = r0 + i;
+    float f[kHitWords];
+#pragma unroll
+    for (uint32_t k = 0; k < kHitWords; ++k) f[k] = rows[(size_t)k * n + g];
+    const uint32_t what = __float_as_uint(f[11]);
+    uint32_t *o = t + kHitWords * i;  // stride 13: conflict-free
+    o[0] = what == BZR_WHAT_INTERSECT ? 1u : 0u;  // mValid
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) o[1 + k] = __float_as_uint(f[1 + k]);  // point, cos
+    o[5] = __float_as_uint(f[0]);                                          // distance
+#pragma unroll
+    for (uint32_t k = 0; k < 6; ++k) o[6 + k] = __float_as_uint(f[5 + k]);  // bary, normal
+    o[12] = what;
+    if (patch) patch[g] = __float_as_uint(f[12]);
+  }
+  __syncthreads();
+  for (uint32_t w = i; w < kHitWords * m; w += kPackThreads) rec[kHitWords * r0 + w] = t[w];
+}
+
 bzr_status fail(bzr_status s, const std::string &msg) {
   bzr_internal_set_error(msg.c_str());
   return s;
 }
 
 }  // namespace
+
+hipError_t bzr_hits_to_records(hipStream_t stream, const float *rows, uint32_t n, void *records, uint32_t *patch) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_hits_to_records, dim3((n + kPackThreads - 1) / kPackThreads), dim3(kPackThreads), 0, stream,
+                     rows, n, static_cast<uint32_t *>(records), patch);
+  return hipGetLastError();
+}
 
 hipError_t bzr_rays_relayout(hipStream_t stream, const float *src, float *dst, uint32_t n, bool to_soa) {
   if (n == 0) return hipSuccess;

@@ -3451,6 +3451,33 @@ extern "C" bzr_status bzr_mesh_size(const bzr_mesh *mesh, uint32_t *n) {
   return BZR_OK;
 }
 
+// BezierMesh::intersect of n rays given as device rows into device hit rows [13][n]: the body of bzr_intersect
+// and bzr_intersect_records, on the context's stream.
+static bzr_status intersect_rows(bzr_ctx *ctx, const bzr_mesh *mesh, const float *d_rays, uint32_t n, float *d_hits,
+                                 uint32_t flags) {
+  MeshView mv = view_of(mesh);
+  if (use_scan(flags)) {
+    launch(ctx, BZR_KERNEL_INTERSECT_SCAN, k_intersect_scan, dim3(grid_for(n)), mv, d_rays, n, d_hits);
+  } else if (!use_staged(flags, n, mesh->n)) {
+    TraceJob job{};
+    job.rays = d_rays;
+    job.hits = d_hits;
+    job.n = job.ld = n;
+    if (bzr_status s = run_fused<kModeHits>(ctx, single_lens(mv), job, flags)) return s;
+  } else {
+    Work w;
+    const uint32_t ch = chunk_for(ctx, n);
+    if (bzr_status s = ensure_work(ctx, ch, mesh->n, w)) return s;
+    Out o{};
+    o.hits = d_hits;
+    for (uint32_t off = 0; off < n; off += ch)
+      if (bzr_status s = run_segment<kModeHits>(use_fast(flags), ctx, mv, d_rays, n, off, std::min(ch, n - off), nullptr, o, w))
+        return s;
+  }
+  BZR_HIP(hipGetLastError());
+  return BZR_OK;
+}
+
 extern "C" bzr_status bzr_intersect(bzr_ctx *ctx, const bzr_mesh *mesh, const float *rays, uint32_t n, float *hits,
                                     uint32_t flags) {
   if (bzr_status s = check_flags(flags, true)) return s;
@@ -3473,28 +3500,50 @@ extern "C" bzr_status bzr_intersect(bzr_ctx *ctx, const bzr_mesh *mesh, const fl
     if (bzr_status s = rays_in(ctx, rays, r, n, host, aos, tmp)) return s;
     d_rays = r;
   }
-  MeshView mv = view_of(mesh);
-  if (use_scan(flags)) {
-    launch(ctx, BZR_KERNEL_INTERSECT_SCAN, k_intersect_scan, dim3(grid_for(n)), mv, d_rays, n, d_hits);
-  } else if (!use_staged(flags, n, mesh->n)) {
-    TraceJob job{};
-    job.rays = d_rays;
-    job.hits = d_hits;
-    job.n = job.ld = n;
-    if (bzr_status s = run_fused<kModeHits>(ctx, single_lens(mv), job, flags)) return s;
-  } else {
-    Work w;
-    const uint32_t ch = chunk_for(ctx, n);
-    if (bzr_status s = ensure_work(ctx, ch, mesh->n, w)) return s;
-    Out o{};
-    o.hits = d_hits;
-    for (uint32_t off = 0; off < n; off += ch)
-      if (bzr_status s = run_segment<kModeHits>(use_fast(flags), ctx, mv, d_rays, n, off, std::min(ch, n - off), nullptr, o, w))
-        return s;
-  }
-  BZR_HIP(hipGetLastError());
+  if (bzr_status s = intersect_rows(ctx, mesh, d_rays, n, d_hits, flags)) return s;
   if (host) {
     BZR_HIP(hipMemcpyAsync(hits, d_hits, (size_t)n * 13 * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
+    BZR_HIP(hipStreamSynchronize(ctx->stream));
+  }
+  return BZR_OK;
+}
+
+extern "C" bzr_status bzr_intersect_records(bzr_ctx *ctx, const bzr_mesh *mesh, const float *rays, uint32_t n,
+                                            bzr_hit_record *records, uint32_t *patch_index, uint32_t flags) {
+  if (bzr_status s = check_flags(flags, true)) return s;
+  if (bzr_status s = check_ctx_mesh(ctx, mesh)) return s;
+  if (n == 0) return BZR_OK;
+  if (!rays || !records) return set_error(BZR_ERR_INVALID_ARGUMENT, "null buffer");
+  DeviceGuard g(ctx->device);
+  const bool host = !(flags & BZR_DEVICE_PTRS), aos = (flags & BZR_RAYS_AOS) != 0;
+  // staging: the rays' rows (unless the caller's device rows are used as they are), the hit rows, and for host
+  // callers the records and patch words before their copies
+  const size_t rb = (size_t)n * 24, hb = (size_t)n * 52, pb = (size_t)n * 4;
+  const bool stage_rays = host || aos;
+  if (bzr_status s = ensure_buffer(ctx->scratch, ctx->scratch_bytes,
+                                   (stage_rays ? round256(rb) : 0) + (host && aos ? round256(rb) : 0) + round256(hb) +
+                                       (host ? round256(hb) + round256(pb) : 0)))
+    return s;
+  Staging st{static_cast<char *>(ctx->scratch)};
+  const float *d_rays = rays;
+  if (stage_rays) {
+    float *r = st.take<float>((size_t)n * 6);
+    float *tmp = host && aos ? st.take<float>((size_t)n * 6) : nullptr;
+    if (bzr_status s = rays_in(ctx, rays, r, n, host, aos, tmp)) return s;
+    d_rays = r;
+  }
+  float *d_hits = st.take<float>((size_t)n * 13);
+  void *d_rec = records;
+  uint32_t *d_patch = patch_index;
+  if (host) {
+    d_rec = st.take<uint32_t>((size_t)n * 13);
+    d_patch = patch_index ? st.take<uint32_t>(n) : nullptr;
+  }
+  if (bzr_status s = intersect_rows(ctx, mesh, d_rays, n, d_hits, flags)) return s;
+  BZR_HIP(bzr_hits_to_records(ctx->stream, d_hits, n, d_rec, d_patch));
+  if (host) {
+    BZR_HIP(hipMemcpyAsync(records, d_rec, hb, hipMemcpyDeviceToHost, ctx->stream));
+    if (patch_index) BZR_HIP(hipMemcpyAsync(patch_index, d_patch, pb, hipMemcpyDeviceToHost, ctx->stream));
     BZR_HIP(hipStreamSynchronize(ctx->stream));
   }
   return BZR_OK;

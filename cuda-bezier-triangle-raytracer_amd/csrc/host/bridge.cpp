@@ -59,19 +59,6 @@ float const *records(Ray const *r) { return reinterpret_cast<float const *>(r); 
 float *records(Ray *r) { return reinterpret_cast<float *>(r); }
 uint32_t *words(RefractionResult *s) { return reinterpret_cast<uint32_t *>(s); }
 uint32_t const *words(RefractionResult const *s) { return reinterpret_cast<uint32_t const *>(s); }
-BezierIntersection hitFromSoa(std::vector<float> const &h, std::size_t n, std::size_t i) {
-  BezierIntersection b;
-  b.mIntersection.mDistance = h[i];
-  b.mIntersection.mPoint = Vertex(h[n + i], h[2 * n + i], h[3 * n + i]);
-  b.mIntersection.mCosIncidence = h[4 * n + i];
-  b.mBarycentric = Vertex(h[5 * n + i], h[6 * n + i], h[7 * n + i]);
-  b.mNormal = Vector(h[8 * n + i], h[9 * n + i], h[10 * n + i]);
-  uint32_t what;
-  std::memcpy(&what, &h[11 * n + i], 4);
-  b.mWhat = static_cast<BezierIntersection::What>(what);
-  b.mIntersection.mValid = what == BZR_WHAT_INTERSECT;
-  return b;
-}
 }  // namespace
 
 void traceChain(std::vector<BezierLens const *> const &lenses, Ray const *rays, std::size_t n, Ray *outRays,
@@ -180,13 +167,9 @@ void BezierMesh::intersect(Ray const *rays, std::size_t n, BezierIntersection *o
   bzr_mesh *dm = device(c);
   for (std::size_t off = 0; off < n; off += bzr::kMaxBatch) {
     const std::size_t m = std::min(bzr::kMaxBatch, n - off);
-    std::vector<float> hits(13 * m);
-    bzr::check(bzr_intersect(c.get(), dm, bzr::records(rays + off), static_cast<uint32_t>(m), hits.data(),
-                             BZR_HOST_PTRS | BZR_RAYS_AOS));
-    for (std::size_t i = 0; i < m; ++i) {
-      out[off + i] = bzr::hitFromSoa(hits, m, i);
-      if (patchIndex) std::memcpy(&patchIndex[off + i], &hits[12 * m + i], 4);
-    }
+    bzr::check(bzr_intersect_records(c.get(), dm, bzr::records(rays + off), static_cast<uint32_t>(m),
+                                     reinterpret_cast<bzr_hit_record *>(out + off), patchIndex ? patchIndex + off : nullptr,
+                                     BZR_HOST_PTRS | BZR_RAYS_AOS));
   }
 }
 

@@ -192,6 +192,24 @@ bzr_status bzr_mesh_size(const bzr_mesh *mesh, uint32_t *n);
 /* BezierMesh::intersect over a ray batch (reference/bezierMesh.cpp:206-227). */
 bzr_status bzr_intersect(bzr_ctx *ctx, const bzr_mesh *mesh, const float *rays_soa, uint32_t n,
                          float *hits_soa, uint32_t flags);
+/* One hit in the reference's BezierIntersection layout (reference/bezierTriangle.h:7-21 with
+ * Intersection of reference/3dGeomUtil.h:209-214): 52 bytes, `valid` is the bool mValid in its first
+ * byte (the other three bytes zero). */
+typedef struct bzr_hit_record {
+  uint32_t valid;             /* mIntersection.mValid (what == BZR_WHAT_INTERSECT)   @0  */
+  float    point[3];          /* mIntersection.mPoint                                @4  */
+  float    cos_incidence;     /* mIntersection.mCosIncidence                         @16 */
+  float    distance;          /* mIntersection.mDistance (FLT_MAX on a miss)          @20 */
+  float    bary[3];           /* mBarycentric                                        @24 */
+  float    normal[3];         /* mNormal                                             @36 */
+  uint32_t what;              /* mWhat (BZR_WHAT_*)                                  @48 */
+} bzr_hit_record;
+/* bzr_intersect with the hits written as n bzr_hit_record (the drop-in's BezierIntersection array, no
+ * host-side conversion; the records are built on the device, 52 B per ray) and the hit patch indices in
+ * patch_index [n] (may be NULL; 0xFFFFFFFF on a miss).  Same values as bzr_intersect's rows; flags as
+ * bzr_intersect's, BZR_RAYS_AOS included. */
+bzr_status bzr_intersect_records(bzr_ctx *ctx, const bzr_mesh *mesh, const float *rays, uint32_t n,
+                                 bzr_hit_record *records, uint32_t *patch_index, uint32_t flags);
 /* BezierTriangle::intersect for (patch, ray, limit) triples (reference/bezierTriangle.cpp:123-195).
  * The `patch` field of the output is the input patch index. */
 bzr_status bzr_patch_intersect(bzr_ctx *ctx, const bzr_mesh *mesh, const uint32_t *patch_index,

@@ -480,5 +480,13 @@ class TiledChain {
 
 static_assert(sizeof(BezierTriangle) == sizeof(bzr_patch), "BezierTriangle must match the 264-byte record");
 static_assert(sizeof(Vector) == 12 && sizeof(Matrix) == 36 && sizeof(Plane) == 16, "Eigen-compatible layout");
+static_assert(sizeof(BezierIntersection) == sizeof(bzr_hit_record) &&
+                  offsetof(BezierIntersection, mIntersection.mPoint) == offsetof(bzr_hit_record, point) &&
+                  offsetof(BezierIntersection, mIntersection.mCosIncidence) == offsetof(bzr_hit_record, cos_incidence) &&
+                  offsetof(BezierIntersection, mIntersection.mDistance) == offsetof(bzr_hit_record, distance) &&
+                  offsetof(BezierIntersection, mBarycentric) == offsetof(bzr_hit_record, bary) &&
+                  offsetof(BezierIntersection, mNormal) == offsetof(bzr_hit_record, normal) &&
+                  offsetof(BezierIntersection, mWhat) == offsetof(bzr_hit_record, what),
+              "BezierIntersection must match the 52-byte bzr_hit_record (bzr_intersect_records)");
 
 #endif

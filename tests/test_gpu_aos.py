@@ -110,3 +110,31 @@ def test_tiled_plan_records_frames_in_flight(bzr, ctx, transport, ndev, host):
         assert np.array_equal(_u32(o[0]), _u32(w[0]).T)
         assert np.array_equal(_u32(o[1]), _u32(w[1])) and np.array_equal(_u32(o[2]), _u32(w[2]))
     plan.close()
+
+
+@pytest.mark.parametrize("pipeline", ["fused", "staged", "scan"])
+@pytest.mark.parametrize("device,aos", [(False, False), (False, True), (True, False), (True, True)])
+def test_intersect_records_equal_rows(bzr, ctx, pipeline, device, aos):
+    """bzr_intersect_records: the reference's BezierIntersection records (valid, point, cos, distance, bary,
+    normal, what) and the patch words, field for field the rows of bzr_intersect -- hits and misses."""
+    import torch
+
+    cfg, _, _, lenses = _cfg4(bzr, ctx)
+    rays = grid_rays(cfg, side=128)[:, :12345].copy()
+    mode = {"fused": bzr.PIPELINE_FUSED, "staged": bzr.PIPELINE_STAGED, "scan": bzr.ACCEL_NONE}[pipeline]
+    rows = _u32(bzr.intersect(ctx, lenses[0], rays, mode=mode))
+    arg = np.ascontiguousarray(rays.T) if aos else rays
+    if device:
+        arg = torch.from_numpy(arg).cuda()
+    rec, patch = bzr.intersect_records(ctx, lenses[0], arg, mode=mode | (bzr.RAYS_AOS if aos else 0))
+    if device:
+        torch.cuda.synchronize()
+    rec, patch = _u32(rec), _u32(patch)
+    assert rec.shape == (rays.shape[1], 13)
+    hit = rows[11] == bzr.WHAT_INTERSECT
+    assert 0 < hit.sum() < rays.shape[1]  # hits and misses both present
+    assert np.array_equal(rec[:, 0], hit.astype(np.uint32))
+    assert np.array_equal(rec[:, 1:5], rows[1:5].T)    # point, cos
+    assert np.array_equal(rec[:, 5], rows[0])          # distance
+    assert np.array_equal(rec[:, 6:12], rows[5:11].T)  # bary, normal
+    assert np.array_equal(rec[:, 12], rows[11]) and np.array_equal(patch, rows[12])
