@@ -70,6 +70,7 @@ void traceChain(std::vector<BezierLens const *> const &lenses, Ray const *rays, 
     meshes.push_back(l->getMesh().device(c));
     ri.push_back(l->getRefractiveIndex());
   }
+  std::lock_guard<std::mutex> hold(c.lock());
   for (std::size_t off = 0; off < n; off += kMaxBatch) {
     const std::size_t m = std::min(kMaxBatch, n - off);
     check(bzr_trace_chain(c.get(), meshes.data(), ri.data(), static_cast<uint32_t>(meshes.size()), records(rays + off),
@@ -89,6 +90,11 @@ void traceChainTiled(std::vector<Context *> const &ctxs, std::vector<BezierLens 
     handles.push_back(c->get());
     for (auto const *l : lenses) meshes.push_back(l->getMesh().device(*c));
   }
+  std::vector<Context *> order(ctxs);  // held in id order: two such calls over shared contexts cannot deadlock
+  std::sort(order.begin(), order.end(), [](Context *a, Context *b) { return a->id() < b->id(); });
+  order.erase(std::unique(order.begin(), order.end()), order.end());  // (a repeated context: bzr_trace_tiled says so)
+  std::vector<std::unique_lock<std::mutex>> hold;
+  for (Context *c : order) hold.emplace_back(c->lock());
   if (n > UINT32_MAX) throw std::length_error("traceChainTiled: more than 2^32-1 rays in one call");
   check(bzr_trace_tiled(handles.data(), static_cast<uint32_t>(handles.size()), meshes.data(), ri.data(),
                         static_cast<uint32_t>(lenses.size()), records(rays), static_cast<uint32_t>(n), tileRays,
@@ -165,6 +171,7 @@ void BezierMesh::intersect(Ray const *rays, std::size_t n, BezierIntersection *o
                            bzr::Context *ctx) const {
   bzr::Context &c = ctx ? *ctx : bzr::defaultContext();
   bzr_mesh *dm = device(c);
+  std::lock_guard<std::mutex> hold(c.lock());
   for (std::size_t off = 0; off < n; off += bzr::kMaxBatch) {
     const std::size_t m = std::min(bzr::kMaxBatch, n - off);
     bzr::check(bzr_intersect_records(c.get(), dm, bzr::records(rays + off), static_cast<uint32_t>(m),
@@ -189,6 +196,7 @@ void BezierLens::refract(Ray const *rays, RefractionResult const *expected, std:
                          RefractionResult *outStatus, bzr::Context *ctx) const {
   bzr::Context &c = ctx ? *ctx : bzr::defaultContext();
   bzr_mesh *dm = mMesh.device(c);
+  std::lock_guard<std::mutex> hold(c.lock());
   for (std::size_t off = 0; off < n; off += bzr::kMaxBatch) {
     const std::size_t m = std::min(bzr::kMaxBatch, n - off);
     bzr::check(bzr_refract(c.get(), dm, mRefractiveIndex, bzr::records(rays + off), bzr::words(expected + off), 0u,

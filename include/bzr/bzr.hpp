@@ -27,6 +27,7 @@
 #include <initializer_list>
 #include <limits>
 #include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <type_traits>
@@ -385,10 +386,15 @@ class Context {
   // Process-unique, never reused (a new Context may get a destroyed one's bzr_ctx address).
   uint64_t id() const { return mId; }
   void sync() const;
+  // Held by the batch calls for their whole (synchronous) use of the context: several host threads may share
+  // one context -- e.g. defaultContext() -- and call the batch overloads concurrently, as the reference's hot
+  // methods may be; the calls then run one after another.
+  std::mutex &lock() const { return mLock; }
 
  private:
   bzr_ctx *mCtx = nullptr;
   uint64_t mId = 0;
+  mutable std::mutex mLock;
 };
 void check(bzr_status s);  // throws std::runtime_error with bzr_last_error() text
 struct DeviceMesh;         // device copy of a patch array (bzr_mesh)

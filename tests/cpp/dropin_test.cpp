@@ -8,10 +8,12 @@
 // infrastructure, linked only into this test program); part 4 (only with a HIP device) runs the batch
 // overloads, the chain and the multi-device calls through libbzr and checks them bit-for-bit against the
 // single-ray results and the oracle, and times one ray through each path.
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "3dGeomUtil.h"
@@ -283,6 +285,29 @@ static void hot_path(Mesh const &lensMesh) {
   int chainExits = 0;
   for (auto s : status) chainExits += s == RefractionResult::cOutside;
   CHECK(chainExits > 0);
+  // four host threads sharing the default context, each calling the batch overloads three times: the context's
+  // lock serialises them (its staging buffers are per context), every result equals the sequential one
+  {
+    std::atomic<int> agree{0};
+    std::vector<std::thread> pool;
+    for (int k = 0; k < 4; ++k)
+      pool.emplace_back([&] {
+        for (int rep = 0; rep < 3; ++rep) {
+          std::vector<Ray> o(n);
+          std::vector<RefractionResult> so(n);
+          std::vector<uint32_t> sg(n);
+          bzr::traceChain({&lens}, rays.data(), n, o.data(), so.data(), sg.data());
+          std::vector<BezierIntersection> hb(n);
+          std::vector<uint32_t> hp(n);
+          bezier.intersect(rays.data(), n, hb.data(), hp.data());
+          bool same = so == status && sg == seg && std::memcmp(o.data(), out.data(), n * sizeof(Ray)) == 0 && hp == patch;
+          for (std::size_t r = 0; r < n && same; ++r) same = same_hit(hb[r], batch[r]);
+          agree += same ? 1 : 0;
+        }
+      });
+    for (auto &t : pool) t.join();
+    CHECK(agree == 12);
+  }
   // the same chain dealt over two contexts on device 0, gathered on the device (peer path), tiles of 100 rays
   bzr::Context c0(0), c1(0);
   std::vector<Ray> outT(n);

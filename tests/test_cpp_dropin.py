@@ -9,7 +9,7 @@ from conftest import PKG, REPO
 
 def build(tmp_path):
     exe = tmp_path / "dropin_test"
-    cmd = ["g++", "-O2", "-std=c++17", "-ffp-contract=off", str(REPO / "tests" / "cpp" / "dropin_test.cpp"),
+    cmd = ["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-pthread", str(REPO / "tests" / "cpp" / "dropin_test.cpp"),
            f"-I{REPO / 'include' / 'bzr'}", f"-I{REPO / 'include'}", f"-I{REPO / 'oracle'}",
            f"-L{PKG / 'lib'}", "-lbzr", f"-L{REPO / 'oracle'}", "-loracle",
            f"-Wl,-rpath,{PKG / 'lib'}", f"-Wl,-rpath,{REPO / 'oracle'}", "-o", str(exe)]
