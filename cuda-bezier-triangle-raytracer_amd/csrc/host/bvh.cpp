@@ -943,7 +943,7 @@ extern "C" int32_t bzr_debug_gate_obbs(const void *patches, uint32_t n, uint32_t
   if ((!patches && n) || (!out && n) || stride % 4 || stride < 264) return 1;
   if (tier != bzr_host::kTierFar && tier != bzr_host::kTierNear) return 1;
   bzr_host::Bvh bvh = bzr_host::build_bvh(static_cast<const float *>(patches), n, stride / 4, tier);
-  std::memcpy(out, bvh.patch_obb.data(), (size_t)n * 16 * sizeof(float));
+  std::copy(bvh.patch_obb.begin(), bvh.patch_obb.begin() + (size_t)n * 16, out);  // (memcpy from an empty vector is UB)
   return 0;
   } catch (std::exception const &e) {  // build_bvh's invariant checks: a status, not a throw across the C ABI
     bzr_internal_set_error(e.what());
@@ -1298,7 +1298,7 @@ extern "C" int32_t bzr_debug_always_list(const void *patches, uint32_t n, uint32
   if (tier != bzr_host::kTierFar && tier != bzr_host::kTierNear) return 1;
   bzr_host::Bvh bvh = bzr_host::build_bvh(static_cast<const float *>(patches), n, stride / 4, tier);
   *count = static_cast<uint32_t>(bvh.always.size());
-  if (out) std::memcpy(out, bvh.always.data(), bvh.always.size() * sizeof(uint32_t));
+  if (out) std::copy(bvh.always.begin(), bvh.always.end(), out);
   return 0;
   } catch (std::exception const &e) {  // build_bvh's invariant checks: a status, not a throw across the C ABI
     bzr_internal_set_error(e.what());
@@ -1312,7 +1312,7 @@ extern "C" int32_t bzr_debug_always_wedges(const void *patches, uint32_t n, uint
   if ((!patches && n) || !out || stride % 4 || stride < 264) return 1;
   if (tier != bzr_host::kTierFar && tier != bzr_host::kTierNear) return 1;
   bzr_host::Bvh bvh = bzr_host::build_bvh(static_cast<const float *>(patches), n, stride / 4, tier);
-  std::memcpy(out, bvh.always_wedge.data(), bvh.always_wedge.size() * sizeof(float));
+  std::copy(bvh.always_wedge.begin(), bvh.always_wedge.end(), out);
   return 0;
   } catch (std::exception const &e) {  // build_bvh's invariant checks: a status, not a throw across the C ABI
     bzr_internal_set_error(e.what());
