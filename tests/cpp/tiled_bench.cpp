@@ -13,7 +13,7 @@
 // (tile ty * 64 + tx) for tests/test_cpp_bench.py, which checks them against the committed oracle digests of
 // the whole frame (tests/golden/d_cfg4_4096.npz).
 //
-// Usage: tiled_bench [--frames K] [--warmup W] [--prewarm-s S] [--slots F] [--devices N] [--side S]
+// Usage: tiled_bench [--frames K] [--warmup W] [--prewarm-s S] [--slots F] [--devices N [--one-gpu]] [--side S]
 //                    [--host-frames H] [--dump path]
 // Prints one JSON line.  --host-frames also times H synchronous host-pointer frames (TiledChain::trace into
 // host Rays and bzr::traceChain), whose rates include the PCIe copies and the host AoS <-> SoA conversions.
@@ -47,6 +47,7 @@ constexpr int kTile = 64;
 
 struct Args {
   int frames = 100, warmup = 10, slots = 3, devices = 1, side = 4096, host_frames = 0;
+  bool one_gpu = false;  // --one-gpu: every list device is HIP device 0 (the plan's host work at N shares, one GPU)
   double prewarm_s = 0.3;
   std::string dump;
 };
@@ -63,6 +64,7 @@ Args parse(int argc, char **argv) {
     else if (k == "--warmup") a.warmup = std::stoi(next());
     else if (k == "--slots") a.slots = std::stoi(next());
     else if (k == "--devices") a.devices = std::stoi(next());
+    else if (k == "--one-gpu") a.one_gpu = true;
     else if (k == "--side") a.side = std::stoi(next());
     else if (k == "--host-frames") a.host_frames = std::stoi(next());
     else if (k == "--prewarm-s") a.prewarm_s = std::stod(next());
@@ -141,7 +143,7 @@ int main(int argc, char **argv) {
     std::vector<std::vector<bzr::Context *>> slots(a.slots);
     for (int s = 0; s < a.slots; ++s)
       for (int d = 0; d < a.devices; ++d) {
-        owned.push_back(std::make_unique<bzr::Context>(d));
+        owned.push_back(std::make_unique<bzr::Context>(a.one_gpu ? 0 : d));
         slots[s].push_back(owned.back().get());
       }
     t0 = now();
@@ -185,7 +187,12 @@ int main(int argc, char **argv) {
     plan.sync();
     const int first_timed = frame;
     t0 = now();
-    for (int k = 0; k < a.frames; ++k) trace();
+    double enqueue_s = 0.0;  // host time inside TiledChain::trace (the launches and copies it queues per frame)
+    for (int k = 0; k < a.frames; ++k) {
+      const double tq = now();
+      trace();
+      enqueue_s += now() - tq;
+    }
     plan.sync();
     const double elapsed = now() - t0;
     const double ms = elapsed / a.frames * 1e3, mrays = static_cast<double>(segments) * a.frames / elapsed / 1e6;
@@ -240,14 +247,15 @@ int main(int argc, char **argv) {
     const char *tp_name[] = {"auto", "rccl", "peer", "direct"};
     const int tp = plan.transport();
     std::printf("{\"metric\": \"Mrays/sec (primary+refracted), C++ host path (bzr::TiledChain)\", \"value\": %.3f, "
-                "\"unit\": \"Mrays/s\", \"ms_per_frame\": %.4f, \"frames\": %d, \"warmup\": %d, \"prewarm_s\": %.2f, "
+                "\"unit\": \"Mrays/s\", \"ms_per_frame\": %.4f, \"host_enqueue_ms_per_frame\": %.4f, \"frames\": %d, "
+                "\"warmup\": %d, \"prewarm_s\": %.2f, "
                 "\"slots\": %d, \"devices\": %d, \"transport\": \"%s\", \"side\": %d, \"primaries\": %zu, "
                 "\"segments_per_frame\": %llu, \"preprocess_s\": %.3f, \"plan_create_s\": %.3f, \"set_rays_s\": %.3f, "
                 "\"host_frames\": %d, \"host_tiled_ms_per_frame\": %.3f, \"host_tiled_mrays\": %.3f, "
                 "\"host_trace_chain_ms_per_frame\": %.3f, \"host_trace_chain_mrays\": %.3f, "
                 "\"gpu_max_hw_queues\": \"%s\", \"workload\": \"cfg4: two makeEllipsoid(32,16,(1,4,2)) lenses at x=10 "
                 "and x=13, ri 1.3, centre-first 64x64 tiles\"}\n",
-                mrays, ms, a.frames, a.warmup, a.prewarm_s, a.slots, a.devices, tp_name[tp & 3], a.side, n,
+                mrays, ms, enqueue_s / a.frames * 1e3, a.frames, a.warmup, a.prewarm_s, a.slots, a.devices, tp_name[tp & 3], a.side, n,
                 static_cast<unsigned long long>(segments), prep_s, plan_s, set_rays_s, a.host_frames, host_tiled_ms,
                 host_tiled_ms > 0 ? segments / (host_tiled_ms * 1e3) : 0.0, host_chain_ms,
                 host_chain_ms > 0 ? segments / (host_chain_ms * 1e3) : 0.0, std::getenv("GPU_MAX_HW_QUEUES"));
