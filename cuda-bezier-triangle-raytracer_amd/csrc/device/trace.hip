@@ -1746,13 +1746,17 @@ template <int kMode, bool kFast>
 #else
 #define BZR_RESOLVE_ATTR
 #endif
-// BZR_FINISH_NORAY (A/B knob, default 0): the intersect segments' k_finish reads no ray -- a BezierIntersection
-// needs none -- and the overflow rays (whose winner k_finish would evaluate again, with the ray) are emitted by
-// k_finish_ovf just before it; 24 B per ray less of an HBM-bound kernel, one launch more per chunk.  cfg5 frames
-// +0.6 %, cfg3 -0.6 to -1 % with frames in flight, the finish pair slower on lone frames
-// (profiles/r05_ab_finish_noray.jsonl): not kept.
+// BZR_FINISH_NORAY (default 1; 0 = the round-4 k_finish): the intersect segments' k_finish reads no ray -- a
+// BezierIntersection needs none -- and the overflow rays (whose winner k_finish would evaluate again, with the ray)
+// are emitted by k_finish_ovf just before it; 24 B per ray less, one small launch more per chunk.  First measured
+// with the count tested before the key was loaded (the key and slot loads then waited on it): cfg5 +0.6 %, cfg3
+// -0.6 to -1 % with frames in flight, lone frames slower (profiles/r05_ab_finish_noray.jsonl).  With count and
+// key loaded together: lone frames cfg5 -0.5 %, cfg3 -1.2 %; frames in flight cfg5 +-0.3 %, cfg3 +1.9 %
+// (profiles/r05_ab_finish_noray_v2.jsonl), same bits; the intersect k_finish drops from 112 to 12 VGPRs (the
+// overflow rays' re-evaluation moved out).  Its HBM reads did not move (385.7 MB per 8 M-ray cfg5 chunk either
+// way, profiles/r05_cfg5_staged_noray.txt): the rays it no longer reads were hits in the 256 MB MALL.  Kept.
 #ifndef BZR_FINISH_NORAY
-#define BZR_FINISH_NORAY 0
+#define BZR_FINISH_NORAY 1
 #endif
 __global__ __launch_bounds__(kBlock) BZR_FINISH_ATTR void k_finish(MeshView m, const float *rays, uint32_t ld, uint32_t off, uint32_t n,
                                                    Work w, Out o) {
@@ -1761,8 +1765,10 @@ __global__ __launch_bounds__(kBlock) BZR_FINISH_ATTR void k_finish(MeshView m, c
   if (i >= n) return;
   const uint32_t gi = off + i;
   if constexpr (kMode == kModeHits && BZR_FINISH_NORAY) {
-    if (w.count[i] > kMaxCand) return;  // an overflow ray: k_finish_ovf emitted it
+    // count and key together (testing the count first would make the key and slot loads wait on it)
+    const uint32_t c = w.count[i];
     const unsigned long long k = w.key[i];
+    if (c > kMaxCand) return;  // an overflow ray: k_finish_ovf emitted it
     Hit h = no_hit();
     uint32_t patch = 0xFFFFFFFFu;
     if (k != ~0ull) {
