@@ -1754,7 +1754,8 @@ template <int kMode, bool kFast>
 // key loaded together: lone frames cfg5 -0.5 %, cfg3 -1.2 %; frames in flight cfg5 +-0.3 %, cfg3 +1.9 %
 // (profiles/r05_ab_finish_noray_v2.jsonl), same bits; the intersect k_finish drops from 112 to 12 VGPRs (the
 // overflow rays' re-evaluation moved out).  Its HBM reads did not move (385.7 MB per 8 M-ray cfg5 chunk either
-// way, profiles/r05_cfg5_staged_noray.txt): the rays it no longer reads were hits in the 256 MB MALL.  Kept.
+// way, profiles/r05_cfg5_staged_noray.txt): the compiler had already sunk the old kernel's ray loads into its
+// overflow branch (its ISA loads count and key, then the slot).  Kept for the VGPRs and the lone frames.
 #ifndef BZR_FINISH_NORAY
 #define BZR_FINISH_NORAY 1
 #endif
