@@ -135,18 +135,28 @@ __global__ __launch_bounds__(kPackThreads) void k_compact_scatter(const float *_
 
 // BZR_RAYS_AOS: the reference's Ray records ([n][6]: start xyz, direction xyz, 24 bytes) <-> the kernels'
 // rows ([6][n]).  A block moves 256 rays' 6 KB through LDS so that both sides are read and written
-// contiguously (6 coalesced rounds each); stride 6 in LDS is a 2-way bank conflict.  HBM-bound: 48 bytes
-// per ray.
+// contiguously; stride 6 in LDS is a 2-way bank conflict.  HBM-bound: 48 bytes per ray.  The record side moves
+// 8-byte pairs (3 per thread; a ray is 3 of them) when the records are 8-byte aligned, else single words.
 constexpr uint32_t kRayWords = 6;
+template <bool kPairs>
 __global__ __launch_bounds__(kPackThreads) void k_rays_aos_to_soa(const float *__restrict__ aos, uint32_t n,
                                                                   float *__restrict__ soa) {
-  __shared__ float t[kRayWords * kPackThreads];
+  __shared__ __attribute__((aligned(16))) float t[kRayWords * kPackThreads];
   const size_t r0 = (size_t)blockIdx.x * kPackThreads;
   const uint32_t m = static_cast<uint32_t>(min<size_t>(kPackThreads, n - r0));
+  if constexpr (kPairs) {
+    const float2 *src = reinterpret_cast<const float2 *>(aos + kRayWords * r0);
 #pragma unroll
-  for (uint32_t k = 0; k < kRayWords; ++k) {
-    const uint32_t w = k * kPackThreads + threadIdx.x;
-    if (w < kRayWords * m) t[w] = aos[kRayWords * r0 + w];
+    for (uint32_t k = 0; k < kRayWords / 2; ++k) {
+      const uint32_t w = k * kPackThreads + threadIdx.x;
+      if (w < (kRayWords / 2) * m) reinterpret_cast<float2 *>(t)[w] = src[w];
+    }
+  } else {
+#pragma unroll
+    for (uint32_t k = 0; k < kRayWords; ++k) {
+      const uint32_t w = k * kPackThreads + threadIdx.x;
+      if (w < kRayWords * m) t[w] = aos[kRayWords * r0 + w];
+    }
   }
   __syncthreads();
   if (threadIdx.x < m) {
@@ -154,9 +164,10 @@ __global__ __launch_bounds__(kPackThreads) void k_rays_aos_to_soa(const float *_
     for (uint32_t k = 0; k < kRayWords; ++k) soa[(size_t)k * n + r0 + threadIdx.x] = t[kRayWords * threadIdx.x + k];
   }
 }
+template <bool kPairs>
 __global__ __launch_bounds__(kPackThreads) void k_rays_soa_to_aos(const float *__restrict__ soa, uint32_t n,
                                                                   float *__restrict__ aos) {
-  __shared__ float t[kRayWords * kPackThreads];
+  __shared__ __attribute__((aligned(16))) float t[kRayWords * kPackThreads];
   const size_t r0 = (size_t)blockIdx.x * kPackThreads;
   const uint32_t m = static_cast<uint32_t>(min<size_t>(kPackThreads, n - r0));
   if (threadIdx.x < m) {
@@ -164,10 +175,19 @@ __global__ __launch_bounds__(kPackThreads) void k_rays_soa_to_aos(const float *_
     for (uint32_t k = 0; k < kRayWords; ++k) t[kRayWords * threadIdx.x + k] = soa[(size_t)k * n + r0 + threadIdx.x];
   }
   __syncthreads();
+  if constexpr (kPairs) {
+    float2 *dst = reinterpret_cast<float2 *>(aos + kRayWords * r0);
 #pragma unroll
-  for (uint32_t k = 0; k < kRayWords; ++k) {
-    const uint32_t w = k * kPackThreads + threadIdx.x;
-    if (w < kRayWords * m) aos[kRayWords * r0 + w] = t[w];
+    for (uint32_t k = 0; k < kRayWords / 2; ++k) {
+      const uint32_t w = k * kPackThreads + threadIdx.x;
+      if (w < (kRayWords / 2) * m) dst[w] = reinterpret_cast<const float2 *>(t)[w];
+    }
+  } else {
+#pragma unroll
+    for (uint32_t k = 0; k < kRayWords; ++k) {
+      const uint32_t w = k * kPackThreads + threadIdx.x;
+      if (w < kRayWords * m) aos[kRayWords * r0 + w] = t[w];
+    }
   }
 }
 
@@ -218,10 +238,15 @@ hipError_t bzr_hits_to_records(hipStream_t stream, const float *rows, uint32_t n
 hipError_t bzr_rays_relayout(hipStream_t stream, const float *src, float *dst, uint32_t n, bool to_soa) {
   if (n == 0) return hipSuccess;
   const dim3 grid((n + kPackThreads - 1) / kPackThreads);
-  if (to_soa)
-    hipLaunchKernelGGL(k_rays_aos_to_soa, grid, dim3(kPackThreads), 0, stream, src, n, dst);
+  const bool pairs = (reinterpret_cast<uintptr_t>(to_soa ? src : dst) & 7u) == 0u;  // the records' alignment
+  if (to_soa && pairs)
+    hipLaunchKernelGGL(k_rays_aos_to_soa<true>, grid, dim3(kPackThreads), 0, stream, src, n, dst);
+  else if (to_soa)
+    hipLaunchKernelGGL(k_rays_aos_to_soa<false>, grid, dim3(kPackThreads), 0, stream, src, n, dst);
+  else if (pairs)
+    hipLaunchKernelGGL(k_rays_soa_to_aos<true>, grid, dim3(kPackThreads), 0, stream, src, n, dst);
   else
-    hipLaunchKernelGGL(k_rays_soa_to_aos, grid, dim3(kPackThreads), 0, stream, src, n, dst);
+    hipLaunchKernelGGL(k_rays_soa_to_aos<false>, grid, dim3(kPackThreads), 0, stream, src, n, dst);
   return hipGetLastError();
 }
 

@@ -138,3 +138,25 @@ def test_intersect_records_equal_rows(bzr, ctx, pipeline, device, aos):
     assert np.array_equal(rec[:, 5], rows[0])          # distance
     assert np.array_equal(rec[:, 6:12], rows[5:11].T)  # bary, normal
     assert np.array_equal(rec[:, 12], rows[11]) and np.array_equal(patch, rows[12])
+
+
+def test_records_at_an_odd_word_offset(bzr, ctx):
+    """Device records 4 bytes past an 8-byte boundary take the single-word transposes (the 8-byte path needs
+    aligned records); same bits as rows."""
+    import torch
+
+    cfg, _, ri, lenses = _cfg4(bzr, ctx)
+    rays = grid_rays(cfg, side=128)[:, :5001].copy()
+    n = rays.shape[1]
+    want = bzr.trace_chain(ctx, lenses, ri, rays)
+    buf_in = torch.zeros(6 * n + 1, device="cuda")
+    buf_in[1:] = torch.from_numpy(np.ascontiguousarray(rays.T).reshape(-1)).cuda()
+    buf_out = torch.zeros(6 * n + 1, device="cuda")
+    rec_in, rec_out = buf_in[1:].view(n, 6), buf_out[1:].view(n, 6)
+    assert rec_in.data_ptr() % 8 == 4 and rec_out.data_ptr() % 8 == 4
+    st = torch.empty(n, dtype=torch.int32, device="cuda")
+    sg = torch.empty(n, dtype=torch.int32, device="cuda")
+    bzr.trace_chain(ctx, lenses, ri, rec_in, rec_out, st, sg, mode=bzr.RAYS_AOS)
+    torch.cuda.synchronize()
+    assert np.array_equal(_u32(rec_out), _u32(want[0]).T)
+    assert np.array_equal(_u32(st), _u32(want[1])) and np.array_equal(_u32(sg), _u32(want[2]))
