@@ -29,8 +29,8 @@ def _lens(bzr, seed):
     rng = np.random.default_rng(1000 + seed)
     m = bzr.TriMesh()
     sectors, belts = int(rng.integers(3, 41)), int(rng.integers(2, 25))
-    # the revolution axis keeps size 1 (other axis sizes make the reference's welding refuse the ring vertices);
-    # the shape is then stretched, rotated and moved by the random transform
+    # x size 1: makeEllipsoid applies aSize(0) twice (reference/mesh.cpp:456-460), so any other x leaves cracks the
+    # reference's standardizeNormals refuses (tests/test_host_parity.py); the random transform stretches instead
     size = (1.0, float(rng.integers(1, 6)), float(rng.integers(1, 6)))
     if seed % 3 == 2:
         m.make_solid_of_revolution(sectors, belts, bzr.ENVELOPE_TESTLENS, size)

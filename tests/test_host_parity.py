@@ -119,3 +119,39 @@ def test_makeEllipsoid_nonunit_x_is_not_watertight(bzr):
     x != 1 leaves cracks and standardizeNormals throws -- reproduced, not "fixed"."""
     with pytest.raises(bzr.BzrError, match="Vertex on edge"):
         bzr.TriMesh().make_ellipsoid(8, 4, (2, 1, 1)).standardize()
+
+
+@pytest.mark.parametrize("seed", list(range(12)))
+def test_random_recipes_bit_identical(bzr, orc, seed):
+    """The fuzz lenses' recipe (tests/test_gpu_fuzz.py: random sectors, belts and sizes -- x sizes other than 1
+    too, which the reference refuses -- the test-lens envelope, a random stretch, rotation and displacement):
+    product and oracle agree on refusing, and otherwise on every triangle, neighbour and patch word."""
+    rng = np.random.default_rng(7000 + seed)
+    sectors, belts = int(rng.integers(3, 41)), int(rng.integers(2, 25))
+    size = (1.0 if seed % 4 else float(rng.integers(2, 4)), float(rng.integers(1, 6)), float(rng.integers(1, 6)))
+    q = rng.normal(size=4)
+    w, x, y, z = q / np.linalg.norm(q)
+    rot = np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w)],
+                    [2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w)],
+                    [2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)]], np.float32)
+    rot *= np.float32(rng.uniform(0.5, 3.0))
+    disp = rng.uniform(-20, 20, 3)
+    out = []
+    for cls in (bzr.TriMesh, orc.OMesh):
+        m = cls()
+        if seed % 3 == 2:
+            m.make_solid_of_revolution(sectors, belts, bzr.ENVELOPE_TESTLENS, size)
+        else:
+            m.make_ellipsoid(sectors, belts, size)
+        m.transform(rot, disp)
+        try:
+            m.standardize()
+            out.append((m.triangles, m.neighbours(), m.bezier_patches()))
+        except (bzr.BzrError, RuntimeError) as e:
+            assert "Vertex on edge" in str(e)
+            out.append(None)
+    a, b = out
+    assert (a is None) == (b is None)
+    if a is not None:
+        assert same(a[0], b[0]) and np.array_equal(a[1][0], b[1][0]) and np.array_equal(a[1][1], b[1][1])
+        assert same(a[2], b[2])
