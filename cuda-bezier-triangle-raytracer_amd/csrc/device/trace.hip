@@ -151,6 +151,16 @@ __device__ __forceinline__ uint32_t deal_blocks(uint32_t b, uint32_t nblocks) {
 #define BZR_TRAV_BLOCK 64
 #endif
 constexpr uint32_t kAblockMin = 64, kAblockMax = 1024, kAblockBlock = 256;
+// BZR_TRAV_ALDS (A/B knob, default 0): with the block pre-test (BZR_TRAV_ABLOCK 1), the block copies its kept
+// always-listed records (the 96 bytes the per-lane gate reads) into LDS once, so the waves' per-lane gates read
+// them there instead of waiting on one scalar load each (when at most kAldsMax are kept; else as before).
+// Same 64 VGPRs and 8 waves, 18 KB of LDS per block; cfg5 k_traverse 3.85 -> 3.93 ms per lone frame, bench lines
+// -0.8 % (profiles/r05_ab_traverse_alds.jsonl): the scalar loads hit the scalar cache; the copy and the records as
+// VGPR operands cost more.  Not kept.
+#ifndef BZR_TRAV_ALDS
+#define BZR_TRAV_ALDS 0
+#endif
+constexpr uint32_t kAldsMax = 128, kAldsQuads = 6;
 constexpr int kTravBlock = BZR_TRAV_BLOCK;
 // BZR_SLAB_FMA (default 1): the traversal slab test as fma(lo, inv, -s*inv) (mirrored by bvh.cpp slab_h).
 #ifndef BZR_SLAB_FMA
@@ -658,6 +668,28 @@ __device__ __forceinline__ bool always_gate(const float4 *always, uint32_t k, bo
   const u32x8 wq = *((const cu32x8 *)(uintptr_t)(always + (size_t)kAlwaysQuads * k + 4));
   return always_gate_rec(r, wq, act, s, d, patch);
 }
+// The same gate from a record staged in LDS (BZR_TRAV_ALDS): quads 0-3 the leaf record, 4-5 the wedge words.
+__device__ __forceinline__ bool always_gate_lds(const float4 *q, bool act, f3 s, f3 d, uint32_t &patch) {
+  u32x16 r;
+  u32x8 wq;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float4 v = q[k];
+    r[4 * k] = __float_as_uint(v.x);
+    r[4 * k + 1] = __float_as_uint(v.y);
+    r[4 * k + 2] = __float_as_uint(v.z);
+    r[4 * k + 3] = __float_as_uint(v.w);
+  }
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const float4 v = q[4 + k];
+    wq[4 * k] = __float_as_uint(v.x);
+    wq[4 * k + 1] = __float_as_uint(v.y);
+    wq[4 * k + 2] = __float_as_uint(v.z);
+    wq[4 * k + 3] = __float_as_uint(v.w);
+  }
+  return always_gate_rec(r, wq, act, s, d, patch);
+}
 
 // Wave-level pre-test of the always list.  The active rays of a wave form a bundle: origins in the box
 // [slo, shi], directions in [dlo, dhi] (wave min / max, once per segment).  Lane j tests always-listed
@@ -1067,7 +1099,8 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
                                               uint32_t off, const uint32_t *__restrict__ alive, uint32_t n,
                                               const Work &w, unsigned long long *counters, uint32_t i, uint32_t *stk,
                                               float *bl, uint32_t *pend, uint32_t *raw, float *ubl = nullptr,
-                                              unsigned long long *akeep = nullptr, uint32_t *rk = nullptr) {
+                                              unsigned long long *akeep = nullptr, uint32_t *rk = nullptr,
+                                              float4 *arec = nullptr) {
 #if BZR_TRAV_PHASES
   unsigned long long ph_acc[6] = {0ull, 0ull, 0ull, 0ull, 0ull, 0ull}, ph_t = __builtin_amdgcn_s_memtime();
   uint32_t ph_cur = 0;
@@ -1150,6 +1183,24 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
       if ((threadIdx.x & 63u) == 0u) akeep[(base + threadIdx.x) >> 6] = km;
     }
     __syncthreads();
+#if BZR_TRAV_ALDS
+    if constexpr (kAblock == 1) {  // the kept records into LDS, in list order (word, then bit)
+      const uint32_t words = (m.n_always + 63u) / 64u;
+      uint32_t total = 0;
+      for (uint32_t q = 0; q < words; ++q) total += (uint32_t)__popcll(akeep[q]);
+      if (total <= kAldsMax) {
+        for (uint32_t e = threadIdx.x; e < total * kAldsQuads; e += kBlk) {
+          const uint32_t j = e / kAldsQuads, qd = e - j * kAldsQuads;
+          uint32_t q = 0, before = 0;
+          while (before + (uint32_t)__popcll(akeep[q]) <= j) before += (uint32_t)__popcll(akeep[q++]);
+          unsigned long long bits = akeep[q];
+          for (uint32_t k = before; k < j; ++k) bits &= bits - 1ull;  // drop the kept patches before j
+          arec[e] = m.always[(size_t)kAlwaysQuads * (q * 64u + (uint32_t)__builtin_ctzll(bits)) + qd];
+        }
+      }
+      __syncthreads();
+    }
+#endif
   }
   while (bwalk) {
     if (pi < npend) {
@@ -1319,6 +1370,21 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
         }
       }
       } else {
+#if BZR_TRAV_ALDS
+      uint32_t total = 0;
+      for (uint32_t q = 0; q < words; ++q) total += (uint32_t)__popcll(akeep[q]);
+      if (total <= kAldsMax) {
+        for (uint32_t j = 0; j < total; ++j) {
+          uint32_t b;
+          if (counters) {
+            ++c_leaves;
+            c_gates += (uint32_t)__popcll(__ballot(active));
+          }
+          const bool pass = always_gate_lds(arec + (size_t)kAldsQuads * j, active, s, d, b);
+          list_candidate(pass, b, w, n, i, cnt, rpend);
+        }
+      } else
+#endif
       for (uint32_t q = 0; q < words; ++q) {
         for (unsigned long long am = akeep[q]; am; am &= am - 1ull) {
           uint32_t b;
@@ -1506,8 +1572,13 @@ __global__ __launch_bounds__(kBlk) BZR_TRAV_ATTR void k_traverse(MeshView m, con
     static_assert(!kAblock || BZR_TRAV_BUNDLE, "BZR_TRAV_ABLOCK needs the bundle walk");
     __shared__ float ubl[16];                                  // the block's union bundle (words 0..12)
     __shared__ unsigned long long akeep[kAblockMax / 64u];     // block-kept always-listed patches
+#if BZR_TRAV_ALDS
+    __shared__ float4 arec[kAldsMax * kAldsQuads];             // their records (BZR_TRAV_ALDS)
+#else
+    float4 *arec = nullptr;
+#endif
     traverse_rays<kBlk, kAblock>(m, rays, ld, off, alive, n, w, counters, b * kBlk + threadIdx.x, stack[threadIdx.x >> 6],
-                                 bundle[threadIdx.x >> 6], wpend, wraw, ubl, akeep, wrk);
+                                 bundle[threadIdx.x >> 6], wpend, wraw, ubl, akeep, wrk, arec);
   } else {
     traverse_rays<kBlk, 0>(m, rays, ld, off, alive, n, w, counters, b * kBlk + threadIdx.x, stack[threadIdx.x >> 6],
                            bundle[threadIdx.x >> 6], wpend, wraw, nullptr, nullptr, wrk);
