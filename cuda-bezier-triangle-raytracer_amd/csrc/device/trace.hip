@@ -616,14 +616,28 @@ __device__ __forceinline__ uint32_t lanes_below(unsigned long long mask) {
 // (t order, b, j).  A ray's candidates are distinct patches, so for one ray that orders like the reference's
 // (t, scanned patch index) with strict < -- the follow side's hit ranks at its candidate's position, as in
 // reference/bezierMesh.cpp:206-227 (oracle orc_mesh_intersect).
+// BZR_RECORD_RET (default 1; 0 = the round-4 record): take the key's old value back and write the slot only when
+// this pair is the ray's best so far -- the final key's pair always wrote its slot (the minimum is unique), later
+// losers skip their 48 bytes; the wave then waits for the atomic before its stores.  cfg5 per 8 M-ray chunk:
+// k_newton writes 542 -> 450 MB, k_resolve 41 -> 33 MB (profiles/r05_cfg5_staged_recret.txt); time within noise
+// (lone cfg5 +0.4 %, cfg3 -0.1 %; frames in flight cfg5 +0.3 %, cfg3 +1.1 %; profiles/r05_ab_record_ret.jsonl).
+#ifndef BZR_RECORD_RET
+#define BZR_RECORD_RET 1
+#endif
 __device__ __forceinline__ void record(float *__restrict__ slot, uint32_t n, uint32_t ray, uint32_t j, uint32_t b,
                                        const Hit &h, uint32_t src, unsigned long long *key) {
   if (!(h.t < FLT_MAX)) return;
+  const unsigned long long k = ((unsigned long long)t_order(h.t) << 32) | (b << 6) | j;
+#if BZR_RECORD_RET
+  if (!(k < atomicMin(key, k))) return;
+#endif
   float4 *r = reinterpret_cast<float4 *>(slot) + (size_t)3 * ((size_t)j * n + ray);  // AoS: 48 bytes per slot
   r[0] = make_float4(h.t, h.point.x, h.point.y, h.point.z);
   r[1] = make_float4(h.cs, h.bary.x, h.bary.y, h.bary.z);
   r[2] = make_float4(h.normal.x, h.normal.y, h.normal.z, __uint_as_float(src));
-  atomicMin(key, ((unsigned long long)t_order(h.t) << 32) | (b << 6) | j);
+#if !BZR_RECORD_RET
+  atomicMin(key, k);
+#endif
 }
 
 // Word group g of a 64-byte leaf record (planar record, patch index in the last word): q0..q3 of the gate.
