@@ -14,11 +14,14 @@ results bit-identical to the reference restatement (tests/test_gpu_parity.py).  
 ranks as 64x64 tiles round-robin (the north-star's 1->8 GPU scaling on a fixed 4096^2 grid); --scaling
 weak: the image grows to side x (side*N).  Each frame's results are gathered to rank 0 over RCCL inside
 the timed region, double-buffered so frame k's gather overlaps frame k+1's tracing (bzr_amd/frame.py layouts):
---gather compact (the default for the chain configs) every final ray on rank 0 in ~17.6 B per primary: a
-status/segment byte per primary plus the final rays of the primaries that refracted (rank 0 regenerates the
-others from their pixels); --gather rays the 6 final-ray floats + the word (28 B per primary); --gather image
-the per-primary status + segment-count word only (4 B; the default for the intersect configs, whose `what`
-row it carries; the final rays / hits stay in each rank's HBM); --gather none nothing (tracing alone).
+--gather image (the default, "auto") the frame's result image on rank 0: the per-primary status + segment-count
+word (4 B per primary; for the intersect configs the hit's `what` row), the final rays / hits staying in each
+rank's HBM -- at N = 8 on cfg4 ~0.12 ms of xGMI per frame against a 0.58 ms rank frame (DESIGN.md (e) byte
+budget), so the gather never bounds the strong-scaling line; --gather compact every final ray on rank 0 in
+~17.6 B per primary (a status/segment byte per primary plus the final rays of the primaries that refracted;
+rank 0 regenerates the others from their pixels), ~0.49-0.58 ms per frame at N = 8, i.e. as long as the frame
+itself; --gather rays the 6 final-ray floats + the word (28 B per primary; longer than the N = 8 frame);
+--gather none nothing (tracing alone).  The line reports gather_only_ms_per_frame and its ratio to ms_per_step.
 
 --gpus N: N ranks, one process per GPU.  Run bare (no WORLD_SIZE in the environment) with N > 1, bench.py
 starts the N rank processes itself (bzr_amd/launch.py: children with RANK / LOCAL_RANK / WORLD_SIZE and a
@@ -105,7 +108,9 @@ def parse():
     p.add_argument("--scaling", default="strong", choices=["strong", "weak"])
     p.add_argument("--gather", default="auto", choices=["auto", "image", "rays", "compact", "none"],
                    help="what each frame sends to rank 0 when N > 1 (frame.py layouts, DESIGN.md (e) byte budget); "
-                        "auto = compact for the chain configs (every final ray on rank 0), image for intersect")
+                        "auto = image (the result image, 4 B per primary: its gather stays under a fifth of the "
+                        "N = 8 frame); compact = every final ray on rank 0 (~17.6 B per primary, as long as the "
+                        "N = 8 frame)")
     p.add_argument("--accel", default="bvh", choices=["bvh", "none"], help="none = brute-force scan (A/B)")
     p.add_argument("--pipeline", default="fused", choices=["fused", "staged", "auto"],
                    help="culled-path pipeline (include/bzr.h BZR_PIPELINE_*; same output bits): fused = one k_trace "
@@ -356,8 +361,8 @@ def main():
 
     cfg = CONFIGS[a.config]
     chain = cfg.op == "chain"
-    if a.gather == "auto":  # every final ray on rank 0 for the chain; the hit's `what` image for intersect
-        a.gather = "compact" if chain else "image"
+    if a.gather == "auto":  # the frame's result image on rank 0 (the gather that keeps N = 8 margin)
+        a.gather = "image"
     side = a.side or cfg.side
     height = side * world if a.scaling == "weak" else side
     t0 = time.perf_counter()
@@ -640,7 +645,10 @@ def main():
                                   f"{loop.bytes_per_rank / npad:.2f} B per primary ({a.gather})" if gather else ""),
                 "gather": ({"layout": a.gather, "bytes_per_rank_per_frame": loop.bytes_per_rank,
                             "bytes_per_primary": round(loop.bytes_per_rank / npad, 3), "compact_capacity": cap or None,
-                            **verify["gather"]}
+                            **verify["gather"],
+                            # the gather's rate against the frame's: below 1 it never stalls the tracing
+                            "gather_only_over_ms_per_step": (round(verify["gather"]["gather_only_ms_per_frame"] / ms_per_step, 4)
+                                                             if verify["gather"].get("gather_only_ms_per_frame") else None)}
                            if gather else None),
                 "frame_verified": verify["frame"],
                 "pipeline": a.pipeline,
@@ -683,6 +691,15 @@ def main():
                     if work_cnt["newton_rounds"] else None,
                     "newton_lane_utilisation_def": ("(pairs + follow retries) / (64 x k_trace passes)" if fused_kernel
                                                     else "pairs / (64 x k_newton + k_newton_lane chunks)"),
+                    # the fused chain per surface: even segments refract(INSIDE) (a lens's front), odd ones
+                    # refract(OUTSIDE) (its back)
+                    "newton_lane_utilisation_by_surface": ({
+                        "front": round((newton_runs - work_cnt["runs_odd"])
+                                       / max(1, 64 * (work_cnt["newton_rounds"] - work_cnt["rounds_odd"])), 4),
+                        "back": round(work_cnt["runs_odd"] / max(1, 64 * work_cnt["rounds_odd"]), 4),
+                        "passes_front": work_cnt["newton_rounds"] - work_cnt["rounds_odd"],
+                        "passes_back": work_cnt["rounds_odd"]}
+                        if fused_kernel and chain and work_cnt.get("rounds_odd") else None),
                     "overflow_rays_per_frame": work_cnt["overflow_rays"],
                     "source": "GPU counters (bzr_ctx_counters), rank 0, one frame",
                     "oracle_sample_rates": ({"newton": round(cnt["newton"] / cnt["segments"], 4),

@@ -45,7 +45,7 @@ PATCH_WORDS = 66  # sizeof(bzr_patch) / 4
 KERNELS = ("k_traverse", "bucket", "k_newton", "k_follow", "k_finish", "k_overflow", "k_intersect_scan",
            "k_refract_scan", "k_chain_scan", "k_patch", "k_newton_lane", "k_trace")  # BZR_KERNEL_* ids
 COUNTERS = ("segments", "pairs", "follows", "overflow_rays", "lane_chunks", "node_visits", "leaf_fetches",
-            "gate_tests", "newton_rounds")  # BZR_COUNTER_* ids
+            "gate_tests", "newton_rounds", "rounds_odd", "runs_odd")  # BZR_COUNTER_* ids
 HIT_FIELDS = 13
 
 _P = ctypes.c_void_p
@@ -112,6 +112,7 @@ _SIGS = {
     "bzr_bezier_interpolate": [_P, _I32, _P],
     "bzr_pack_frame": [_P, _I32, _P, _P, _P, _U32, _U32, _U32, _P],
     "bzr_debug_unit": [_P, _P, _U32, _P],
+    "bzr_debug_div_heights": [_P, _P, _U32, _P],
     "bzr_debug_wave_clock": [_P, _P, _U32],
     "bzr_debug_wave_clock_rate": [_P, _P, _U32],
 }
@@ -502,6 +503,10 @@ class TiledPlan:
 
             torch.cuda.current_stream(self.ctxs[0][0].device).synchronize()
         _check(lib().bzr_tiled_set_rays(self.handle, r.ptr, (DEVICE_PTRS if r.device else HOST_PTRS) | (mode & RAYS_AOS)))
+        # a device source is only queued for copying (bzr_tiled_set_rays): keep it -- and any contiguous / float32
+        # copy _Buf made of it -- alive until the copy has run, i.e. until the next sync() or set_rays(), so torch's
+        # caching allocator cannot hand its memory to a kernel that overwrites it first
+        self._pending_src = (rays, r) if r.device else None
 
     def trace(self, lenses, ri, out_rays, out_status, out_segments=None, mode=MODE_PARITY):
         """One frame; lenses[d] = device d's DeviceMesh list.  Device tensors (on device 0): queued, ready on
@@ -522,6 +527,7 @@ class TiledPlan:
 
     def sync(self):
         _check(lib().bzr_tiled_sync(self.handle))
+        self._pending_src = None  # the queued ray copy has run
 
     def set_layout(self, layout: str, cap: int = 0):
         """"rays" (28 B per ray) or "compact" (survivors only, up to `cap` per device share)."""

@@ -78,18 +78,20 @@ def build_patches(builder_cls, cfg: Config):
     return [build_lens(builder_cls, lens).bezier_patches() for lens in cfg.lenses]
 
 
-def pixel_coords(cfg: Config, side: int | None = None, order: str = "tiles", tile: int = 8):
+def pixel_coords(cfg: Config, side: int | None = None, order: str = "tiles", tile: int = 8, wave=None):
     """Pixel (row, col) index arrays for a side x side grid.
 
     order "rows": row-major.  order "tiles": tile x tile blocks (one 64-ray wavefront
-    per 8x8 block) so the rays of a wavefront are spatially coherent."""
+    per 8x8 block) so the rays of a wavefront are spatially coherent.  wave=(wr, wc) (order "tiles", wr x wc
+    = the rays per block): blocks of wr rows x wc columns instead (A/B of ray-to-wave mappings)."""
     s = cfg.side if side is None else side
+    wr, wc = (tile, tile) if wave is None else wave
     k = np.arange(s * s, dtype=np.int64)
-    if order == "rows" or s % tile:
+    if order == "rows" or s % wr or s % wc:
         return k // s, k % s
-    t, w = k // (tile * tile), k % (tile * tile)
-    tiles_per_row = s // tile
-    return (t // tiles_per_row) * tile + w // tile, (t % tiles_per_row) * tile + w % tile
+    t, w = k // (wr * wc), k % (wr * wc)
+    tiles_per_row = s // wc
+    return (t // tiles_per_row) * wr + w // wc, (t % tiles_per_row) * wc + w % wc
 
 
 def rays_for(cfg: Config, rows: np.ndarray, cols: np.ndarray, side: int | None = None,
@@ -110,8 +112,8 @@ def rays_for(cfg: Config, rows: np.ndarray, cols: np.ndarray, side: int | None =
     return out
 
 
-def grid_rays(cfg: Config, side: int | None = None, order: str = "tiles") -> np.ndarray:
-    r, c = pixel_coords(cfg, side, order)
+def grid_rays(cfg: Config, side: int | None = None, order: str = "tiles", wave=None) -> np.ndarray:
+    r, c = pixel_coords(cfg, side, order, wave=wave)
     return rays_for(cfg, r, c, side)
 
 

@@ -45,6 +45,7 @@ struct bzr_ctx {
   uint32_t sched_cap = 0;    // waves the buffer holds
   uint32_t sched_waves = 0;  // waves of the call whose order is ready (0: none)
   uint32_t sched_calls = 0;  // calls since the order was first built for this size (rebuilt every BZR_TRACE_SCHED_REFRESH)
+  uint64_t sched_key = 0;    // the order's call: lens set and mode (a different call of the same size rebuilds it)
 };
 
 // BZR_RAYS_AOS (frame_pack.hip): n rays between the reference's [n][6] records and the kernels' [6][n] rows,

@@ -190,6 +190,36 @@ __device__ __forceinline__ f3 unit_or_self(f3 a, float z) {
   return mk(div_rn(a.x, s), div_rn(a.y, s), div_rn(a.z, s));
 #endif
 }
+// BZR_DIV_HEIGHTS (default 1): newton_tail's two bracket quotients din = hIn / cos and dout = hOut / cos
+// (reference/bezierTriangle.cpp:132-133) share their divisor, so they share one refined reciprocal and take the
+// plain fma chain (div_unscaled) -- 3 + 2 x 5 VALU instead of 2 x 11 -- when it provably returns the correctly
+// rounded quotient: the heights are record constants with 2^-40 <= |h| < 2^41 (an exponent test, on the scalar
+// unit when the record sits in SGPRs) and every lane's |cos| lies in [2^-20, 2^20] (the planar gate that let the
+// lane in already requires |cos| >= 1e-5), so V_DIV_SCALE scales nothing (no zero, no denormal divisor,
+// reciprocal or quotient, exponent gap < 96, |num| >= 2^-103) and V_DIV_FIXUP passes the quotient through.
+// Otherwise (a zero height, an extreme lane) both lanes' quotients take the full sequences.  Same bits either
+// way (division sites).
+#ifndef BZR_DIV_HEIGHTS
+#define BZR_DIV_HEIGHTS 1
+#endif
+__device__ __forceinline__ bool height_in_range(float h) {
+  const uint32_t e = (__float_as_uint(h) >> 23) & 0xFFu;  // biased exponent: 2^-40 <= |h| < 2^41
+  return e - (127u - 40u) <= 80u;
+}
+__device__ __forceinline__ void div_heights(float hin, float hout, float ic, float &din, float &dout) {
+#if BZR_DIV_HEIGHTS
+  const bool ok = height_in_range(hin) && height_in_range(hout) && fabsf(ic) >= 0x1p-20f && fabsf(ic) <= 0x1p20f;
+  if (__all(ok)) {
+    const float y0 = __builtin_amdgcn_rcpf(ic);
+    const float y = __builtin_fmaf(__builtin_fmaf(-ic, y0, 1.0f), y0, y0);
+    din = div_unscaled(hin, ic, y);
+    dout = div_unscaled(hout, ic, y);
+    return;
+  }
+#endif
+  din = div_rn(hin, ic);
+  dout = div_rn(hout, ic);
+}
 #include "patch_math_body.inc"
 }  // namespace exact
 
@@ -203,6 +233,10 @@ __device__ __forceinline__ f3 unit_or_self(f3 a, float z) {
   if (!(z > 0.0f)) return a;
   float r = __builtin_amdgcn_rsqf(z);
   return mk(a.x * r, a.y * r, a.z * r);
+}
+__device__ __forceinline__ void div_heights(float hin, float hout, float ic, float &din, float &dout) {
+  din = div_rn(hin, ic);
+  dout = div_rn(hout, ic);
 }
 #include "patch_math_body.inc"
 #pragma clang fp contract(off)

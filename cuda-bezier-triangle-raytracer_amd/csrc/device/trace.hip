@@ -23,6 +23,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <cstdlib>
 #include <functional>
 
 #include <cstdio>
@@ -560,6 +561,8 @@ struct Work {
   void *cub;
   size_t cub_bytes;
   uint32_t cap;      // kMaxCand * chunk
+  uint32_t hbase;    // BZR_TRAV_HYBRID: pair index of the in-wave follow requests' records (j * n + ray past it)
+  uint32_t hyb_t;    // BZR_TRAV_HYBRID: lanes a leaf's gate must pass for its Newton pass to run in the walking wave
 };
 constexpr uint32_t kSlotWords = 12;  // t, point, cos, bary, normal, source patch
 
@@ -624,6 +627,13 @@ __device__ __forceinline__ uint32_t lanes_below(unsigned long long mask) {
 #ifndef BZR_RECORD_RET
 #define BZR_RECORD_RET 1
 #endif
+__device__ __forceinline__ void write_slot(float *__restrict__ slot, uint32_t n, uint32_t ray, uint32_t j, const Hit &h,
+                                           uint32_t src) {
+  float4 *r = reinterpret_cast<float4 *>(slot) + (size_t)3 * ((size_t)j * n + ray);  // AoS: 48 bytes per slot
+  r[0] = make_float4(h.t, h.point.x, h.point.y, h.point.z);
+  r[1] = make_float4(h.cs, h.bary.x, h.bary.y, h.bary.z);
+  r[2] = make_float4(h.normal.x, h.normal.y, h.normal.z, __uint_as_float(src));
+}
 __device__ __forceinline__ void record(float *__restrict__ slot, uint32_t n, uint32_t ray, uint32_t j, uint32_t b,
                                        const Hit &h, uint32_t src, unsigned long long *key) {
   if (!(h.t < FLT_MAX)) return;
@@ -631,10 +641,7 @@ __device__ __forceinline__ void record(float *__restrict__ slot, uint32_t n, uin
 #if BZR_RECORD_RET
   if (!(k < atomicMin(key, k))) return;
 #endif
-  float4 *r = reinterpret_cast<float4 *>(slot) + (size_t)3 * ((size_t)j * n + ray);  // AoS: 48 bytes per slot
-  r[0] = make_float4(h.t, h.point.x, h.point.y, h.point.z);
-  r[1] = make_float4(h.cs, h.bary.x, h.bary.y, h.bary.z);
-  r[2] = make_float4(h.normal.x, h.normal.y, h.normal.z, __uint_as_float(src));
+  write_slot(slot, n, ray, j, h, src);
 #if !BZR_RECORD_RET
   atomicMin(key, k);
 #endif
@@ -1071,9 +1078,47 @@ __device__ __forceinline__ void rank_flush(RankPend &pr, const Work &w, uint32_t
     pr.g = 0ull;
   }
 }
+// BZR_TRAV_HYBRID (A/B knob, default 0 = round 5's k_traverse): in-wave Newton passes for dense leaves (VERDICT r05
+// item 1).  A leaf whose exact planar gate passes for at least Work::hyb_t of the wave's lanes (runtime threshold,
+// BZR_HYBRID_T; 0 = never) is not listed: its patch and lane mask go to the wave's LDS entries (up to kHybEntries;
+// more are listed as before), and once the walk and the always list are done the wave runs one patch-uniform pass
+// per entry with the record in SGPRs (k_trace's site, k_newton's arithmetic: kGated, the lanes passed this gate).
+// A lane keeps its best in-wave (t order, patch) key; it becomes the ray's initial key, with list slot kHybSlot
+// holding its record, so the staged pairs' atomicMin and k_finish treat it like any listed pair's hit.  A follow-side
+// result becomes a follow request for k_resolve on a list slot of its own (cand word kCandFollow: no pair for the
+// ranking or k_place; its pair record at hbase + j n + ray), or, when the list is full, is retried in the wave.
+// Sparse leaves go to the buckets as before.  Same candidates, same keys: the schedule never changes a bit.
+// Measured (cfg5 8192^2 staged, lone frames, scripts/ab.py; profiles/r06_ab_hybrid.jsonl): the in-wave passes
+// cost what the same pairs cost in k_newton (T = 48 with the walk at priority 3: k_traverse +2.02 ms, k_newton
+// -2.0 ms per frame) -- they do not hide behind the walk, which is issue-bound, not latency-bound -- and the
+// compiled-in code alone costs the walk 7.6 % (3.90 -> 4.19 ms at T = 0: 90 SGPR spills, 3 VGPRs to scratch at the
+// 8-wave budget); T = 32 / 16: 13.5 / 17.1 ms per frame against 11.2.  Not kept; same bits in every variant.
+#ifndef BZR_TRAV_HYBRID
+#define BZR_TRAV_HYBRID 0
+#endif
+// BZR_TRAV_PRIO (A/B knob with BZR_TRAV_HYBRID, default 0): the walk at s_setprio(N), the in-wave passes at 0 (as
+// k_trace's BZR_TRACE_PRIO).
+#ifndef BZR_TRAV_PRIO
+#define BZR_TRAV_PRIO 0
+#endif
+#ifndef BZR_HYBRID_T_DEFAULT
+#define BZR_HYBRID_T_DEFAULT 32
+#endif
+static_assert(!BZR_TRAV_HYBRID || BZR_RANK_EARLY == 0, "BZR_TRAV_HYBRID ranks after the walk");
+constexpr uint32_t kHybEntries = 16;
+constexpr uint32_t kListCap = BZR_TRAV_HYBRID ? kMaxCand - 1u : kMaxCand;  // listed slots per ray
+constexpr uint32_t kHybSlot = kMaxCand - 1u;                               // the in-wave winner's list slot
+constexpr uint32_t kCandFollow = 0x80000000u;                             // cand word of an in-wave follow request
+struct HybEntries {  // the wave's dense leaves (LDS)
+  uint32_t *b = nullptr;             // [kHybEntries] patch
+  unsigned long long *g = nullptr;   // [kHybEntries] lanes whose gate passed
+  uint32_t ne = 0u;                  // entries so far (uniform)
+  uint32_t t = 0u;                   // the threshold (Work::hyb_t)
+};
+
 __device__ __forceinline__ void list_candidate(bool pass, uint32_t b, const Work &w, uint32_t n, uint32_t i,
                                                uint32_t &cnt, RankPend &pr) {
-  const bool lst = pass && cnt < kMaxCand;
+  const bool lst = pass && cnt < kListCap;
 #if BZR_RANK_EARLY == 1
   rank_flush(pr, w, n, i, cnt);
 #endif
@@ -1104,22 +1149,44 @@ __device__ __forceinline__ void list_candidate(bool pass, uint32_t b, const Work
   }
 #endif
   if (lst) w.cand[(size_t)cnt * n + i] = b;
-  if (pass) cnt = cnt < kMaxCand ? cnt + 1 : (cnt | kOverflow);
+  if (pass) cnt = cnt < kListCap ? cnt + 1 : (cnt | kOverflow);
+}
+// A leaf's gate result: a dense leaf (BZR_TRAV_HYBRID) becomes one of the wave's entries, any other is listed.
+__device__ __forceinline__ void take_leaf(bool pass, uint32_t b, const Work &w, uint32_t n, uint32_t i, uint32_t &cnt,
+                                          RankPend &pr, HybEntries &hy) {
+#if BZR_TRAV_HYBRID
+  const unsigned long long g = __ballot(pass);
+  if (g == 0ull) return;
+  if (hy.ne < kHybEntries && (uint32_t)__popcll(g) >= hy.t && hy.t != 0u) {
+    if ((threadIdx.x & 63u) == 0u) {
+      hy.b[hy.ne] = b;
+      hy.g[hy.ne] = g;
+    }
+    ++hy.ne;
+    return;
+  }
+#else
+  (void)hy;
+#endif
+  list_candidate(pass, b, w, n, i, cnt, pr);
 }
 // Candidate search.  `alive` (optional): a ray is traced iff alive[off + i] != BZR_RR_NONE.
 // One wave's 64 rays i (lane l of the wave holds ray i); `stk` is the wave's LDS stack.
-template <int kBlk, int kAblock>
+template <int kBlk, int kAblock, bool kFast>
 __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__restrict__ rays, uint32_t ld,
                                               uint32_t off, const uint32_t *__restrict__ alive, uint32_t n,
                                               const Work &w, unsigned long long *counters, uint32_t i, uint32_t *stk,
-                                              float *bl, uint32_t *pend, uint32_t *raw, float *ubl = nullptr,
-                                              unsigned long long *akeep = nullptr, uint32_t *rk = nullptr,
-                                              float4 *arec = nullptr) {
+                                              float *bl, uint32_t *pend, uint32_t *raw, HybEntries hy,
+                                              float *ubl = nullptr, unsigned long long *akeep = nullptr,
+                                              uint32_t *rk = nullptr, float4 *arec = nullptr) {
 #if BZR_TRAV_PHASES
   unsigned long long ph_acc[6] = {0ull, 0ull, 0ull, 0ull, 0ull, 0ull}, ph_t = __builtin_amdgcn_s_memtime();
   uint32_t ph_cur = 0;
 #endif
   uint32_t c_nodes = 0, c_leaves = 0, c_gates = 0;  // work counters (with counters on; wave-uniform)
+#if BZR_TRAV_HYBRID && BZR_TRAV_PRIO
+  __builtin_amdgcn_s_setprio(BZR_TRAV_PRIO);  // the walk's chain of loads ahead of other waves' Newton passes
+#endif
   bool active = i < n && (alive == nullptr || alive[off + i] != BZR_RR_NONE);
   f3 s = mk(0.0f, 0.0f, 0.0f), d = s;
   if (i < n) load_ray(rays, ld, off + i, s, d);
@@ -1233,11 +1300,11 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
         c_leaves += two ? 2u : 1u;
         c_gates += (two ? 2u : 1u) * (uint32_t)__popcll(__ballot(active));
       }
-      list_candidate(active & planar_gate(leaf_q(r0, 0), leaf_q(r0, 1), leaf_q(r0, 2), leaf_q(r0, 3), s, d), r0[15], w,
-                     n, i, cnt, rpend);
+      take_leaf(active & planar_gate(leaf_q(r0, 0), leaf_q(r0, 1), leaf_q(r0, 2), leaf_q(r0, 3), s, d), r0[15], w,
+                     n, i, cnt, rpend, hy);
       if (two)
-        list_candidate(active & planar_gate(leaf_q(r1, 0), leaf_q(r1, 1), leaf_q(r1, 2), leaf_q(r1, 3), s, d), r1[15],
-                       w, n, i, cnt, rpend);
+        take_leaf(active & planar_gate(leaf_q(r1, 0), leaf_q(r1, 1), leaf_q(r1, 2), leaf_q(r1, 3), s, d), r1[15],
+                       w, n, i, cnt, rpend, hy);
 #else
       const uint32_t slot = __builtin_amdgcn_readfirstlane(pend[pi]);
       ++pi;
@@ -1246,8 +1313,8 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
         ++c_leaves;
         c_gates += (uint32_t)__popcll(__ballot(active));
       }
-      list_candidate(active & planar_gate(leaf_q(r, 0), leaf_q(r, 1), leaf_q(r, 2), leaf_q(r, 3), s, d), r[15], w, n,
-                     i, cnt, rpend);
+      take_leaf(active & planar_gate(leaf_q(r, 0), leaf_q(r, 1), leaf_q(r, 2), leaf_q(r, 3), s, d), r[15], w, n,
+                     i, cnt, rpend, hy);
 #endif
       continue;
     }
@@ -1339,7 +1406,7 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
           ++c_leaves;
           c_gates += (uint32_t)__popcll(hm);
         }
-        list_candidate(hit[c] & planar_gate(q0, q1, q2, q3, s, d), r[15], w, n, i, cnt, rpend);
+        take_leaf(hit[c] & planar_gate(q0, q1, q2, q3, s, d), r[15], w, n, i, cnt, rpend, hy);
       } else {
         if (next != 0xFFFFFFFFu) {
           if (sp < kTravStack) stk[sp++] = next;
@@ -1380,7 +1447,7 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
           }
           const uint32_t patch = __builtin_amdgcn_readfirstlane(pend[r0 + __builtin_ctzll(am)]);
           const bool pass = always_gate(m.always, patch, active, s, d, b);
-          list_candidate(pass, b, w, n, i, cnt, rpend);
+          take_leaf(pass, b, w, n, i, cnt, rpend, hy);
         }
       }
       } else {
@@ -1395,7 +1462,7 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
             c_gates += (uint32_t)__popcll(__ballot(active));
           }
           const bool pass = always_gate_lds(arec + (size_t)kAldsQuads * j, active, s, d, b);
-          list_candidate(pass, b, w, n, i, cnt, rpend);
+          take_leaf(pass, b, w, n, i, cnt, rpend, hy);
         }
       } else
 #endif
@@ -1407,7 +1474,7 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
             c_gates += (uint32_t)__popcll(__ballot(active));
           }
           const bool pass = always_gate(m.always, q * 64u + __builtin_ctzll(am), active, s, d, b);
-          list_candidate(pass, b, w, n, i, cnt, rpend);
+          take_leaf(pass, b, w, n, i, cnt, rpend, hy);
         }
       }
       }
@@ -1421,26 +1488,102 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
           c_gates += (uint32_t)__popcll(__ballot(active));
         }
         const bool pass = always_gate(m.always, ab * 64u + __builtin_ctzll(am), active, s, d, b);
-        list_candidate(pass, b, w, n, i, cnt, rpend);
+        take_leaf(pass, b, w, n, i, cnt, rpend, hy);
       }
     }
 
   }
+  // BZR_TRAV_HYBRID: the wave's dense leaves, one patch-uniform Newton pass each (k_trace's site).  A lane's best
+  // (t order, patch) key becomes the ray's initial key (list slot kHybSlot holds its record); a follow-side result
+  // becomes a follow request on a list slot of its own, or is retried here when the list is full.
+  unsigned long long hbest = ~0ull;
+  uint32_t h_pairs = 0u, h_rounds = 0u;  // work counters (uniform)
+#if BZR_TRAV_HYBRID
+  if (hy.ne) {
+    BZR_PHASE(3)
+#if BZR_TRAV_PRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
+    const uint32_t lane = threadIdx.x & 63u;
+    for (uint32_t e = 0; e < hy.ne; ++e) {
+      const uint32_t b = __builtin_amdgcn_readfirstlane(hy.b[e]);
+      const unsigned long long g0 = hy.g[e];
+      const unsigned long long g = ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(g0 >> 32)) << 32) |
+                                   (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)g0);
+      const bool run = lane_bit64(g, lane) && !(cnt & kOverflow);  // (an overflowed lane takes the full scan)
+      if (counters) {
+        h_pairs += (uint32_t)__popcll(__ballot(run));
+        ++h_rounds;
+      }
+      const auto pa = uniform_patch(m.full, b);
+      uint32_t what = kNone;
+      if (run) {
+        const Hit h = patch_intersect<BZR_NEWTON_GATED != 0, kFast>(pa, s, d, false);
+        what = h.what;
+        if (h.what == kIntersect && h.t < FLT_MAX) {
+          const unsigned long long k = ((unsigned long long)t_order(h.t) << 32) | (b << 6) | kHybSlot;
+          if (k < hbest) {
+            hbest = k;
+            write_slot(w.slot, n, i, kHybSlot, h, b);
+          }
+        }
+      }
+      const bool fol = run && what <= kFollow2;
+      if (!__any(fol)) continue;
+      const bool room = fol && cnt < kListCap;
+      const unsigned long long rm = __ballot(room);
+      if (rm) {  // follow requests for k_resolve: pair record (ray | j << 26, b | side << 30) at hbase + j n + ray
+        uint32_t base = 0u;
+        if (lane == 0u) base = atomicAdd(&w.ctr[0], (uint32_t)__popcll(rm));
+        base = __builtin_amdgcn_readfirstlane(base);
+        if (room) {
+          const uint32_t p = w.hbase + cnt * n + i;
+          w.pairs[p] = make_uint2(i | (cnt << 26), b | (what << 30));
+          w.cand[(size_t)cnt * n + i] = kCandFollow;
+          w.fol[base + lanes_below(rm)] = p;
+          ++cnt;
+        }
+      }
+      for (uint32_t side = 0; side < 3u; ++side) {  // list full: the retry runs here (cNone, ranked at b)
+        const bool fl = fol && !room && what == side;
+        if (!__any(fl)) continue;
+        const uint32_t nb = __float_as_uint(pa.r[rec::kNeigh + side]);
+        const auto pn = uniform_patch(m.full, nb);
+        if (counters) {
+          h_pairs += (uint32_t)__popcll(__ballot(fl));
+          ++h_rounds;
+        }
+        if (fl) {
+          const Hit h = patch_intersect<false, kFast>(pn, s, d, true);
+          if (h.what == kIntersect && h.t < FLT_MAX) {
+            const unsigned long long k = ((unsigned long long)t_order(h.t) << 32) | (b << 6) | kHybSlot;
+            if (k < hbest) {
+              hbest = k;
+              write_slot(w.slot, n, i, kHybSlot, h, nb);
+            }
+          }
+        }
+      }
+    }
+  }
+#endif
   if (counters) {  // rays traced (one atomic per wave: on one address, so only with counters on)
     const unsigned long long traced = __ballot(i < n && (alive == nullptr || alive[off + i] != BZR_RR_NONE));
     if ((threadIdx.x & 63u) == 0 && traced) atomicAdd(&w.ctr[2], (uint32_t)__popcll(traced));
-    // walk work (bzr_ctx_counters node_visits / leaf_fetches / gate_tests), spread over the replicas
+    // walk work (bzr_ctx_counters node_visits / leaf_fetches / gate_tests), spread over the replicas; the in-wave
+    // Newton passes' pairs and passes (BZR_TRAV_HYBRID)
     const uint32_t lane = threadIdx.x & 63u, rep = (i >> 6) % kCounterReplicas;
-    const uint32_t v = lane == 0u ? c_nodes : (lane == 1u ? c_leaves : c_gates);
-    const uint32_t which = lane == 0u ? BZR_COUNTER_NODE_VISITS : (lane == 1u ? BZR_COUNTER_LEAF_FETCHES : BZR_COUNTER_GATE_TESTS);
-    if (!BZR_TRAV_PHASES && lane < 3u && v) atomicAdd(&counters[(size_t)rep * BZR_COUNTER_COUNT + which], (unsigned long long)v);
+    const uint32_t v = lane == 0u ? c_nodes : lane == 1u ? c_leaves : lane == 2u ? c_gates : lane == 3u ? h_pairs : h_rounds;
+    const uint32_t which = lane == 0u ? BZR_COUNTER_NODE_VISITS : lane == 1u ? BZR_COUNTER_LEAF_FETCHES
+                           : lane == 2u ? BZR_COUNTER_GATE_TESTS : lane == 3u ? BZR_COUNTER_PAIRS : BZR_COUNTER_NEWTON_ROUNDS;
+    if (!BZR_TRAV_PHASES && lane < 5u && v) atomicAdd(&counters[(size_t)rep * BZR_COUNTER_COUNT + which], (unsigned long long)v);
   }
 #if BZR_RANK_EARLY == 1
   rank_flush(rpend, w, n, i, cnt);
 #endif
   if (i >= n) return;
   w.count[i] = cnt;
-  w.key[i] = ~0ull;
+  w.key[i] = cnt > kMaxCand ? ~0ull : hbest;
   if (cnt > kMaxCand) w.ovf[atomicAdd(&w.ctr[1], 1u)] = i;
 #if BZR_RANK_EARLY == 3
   const uint32_t lane = threadIdx.x & 63u;
@@ -1485,10 +1628,10 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
   for (uint32_t j0 = 0; __any(j0 < listed); j0 += kRankBatch) {
     uint32_t b[kRankBatch], leader[kRankBatch], below[kRankBatch], base[kRankBatch];
 #pragma unroll
-    for (int k = 0; k < kRankBatch; ++k) b[k] = j0 + k < listed ? w.cand[(size_t)(j0 + k) * n + i] : 0u;
+    for (int k = 0; k < kRankBatch; ++k) b[k] = j0 + k < listed ? w.cand[(size_t)(j0 + k) * n + i] : kCandFollow;
 #pragma unroll
     for (int k = 0; k < kRankBatch; ++k) {
-      const bool pend = j0 + k < listed;
+      const bool pend = !(b[k] & kCandFollow);  // (an in-wave follow request is no pair: BZR_TRAV_HYBRID)
       unsigned long long group = 0ull;
       bool todo = pend;
       for (;;) {
@@ -1510,7 +1653,7 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
 #pragma unroll
     for (int k = 0; k < kRankBatch; ++k) {
       const uint32_t bs = __shfl(base[k], (int)leader[k], 64);
-      if (j0 + k < listed) w.rank[(size_t)(j0 + k) * n + i] = bs + below[k];
+      if (!(b[k] & kCandFollow)) w.rank[(size_t)(j0 + k) * n + i] = bs + below[k];
     }
   }
 #else
@@ -1557,7 +1700,7 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
 #else
 #define BZR_TRAV_ATTR
 #endif
-template <int kBlk, int kAblock>
+template <int kBlk, int kAblock, bool kFast>
 __global__ __launch_bounds__(kBlk) BZR_TRAV_ATTR void k_traverse(MeshView m, const float *__restrict__ rays, uint32_t ld,
                                                          uint32_t off, const uint32_t *__restrict__ alive, uint32_t n,
                                                          Work w, unsigned long long *counters) {
@@ -1582,6 +1725,14 @@ __global__ __launch_bounds__(kBlk) BZR_TRAV_ATTR void k_traverse(MeshView m, con
 #else
   uint32_t *wrk = nullptr;
 #endif
+  HybEntries hy;  // the wave's dense leaves (BZR_TRAV_HYBRID)
+#if BZR_TRAV_HYBRID
+  __shared__ uint32_t hyb_b[kBlk / 64][kHybEntries];
+  __shared__ unsigned long long hyb_g[kBlk / 64][kHybEntries];
+  hy.b = hyb_b[threadIdx.x >> 6];
+  hy.g = hyb_g[threadIdx.x >> 6];
+  hy.t = w.hyb_t;
+#endif
   if constexpr (kAblock != 0) {
     static_assert(!kAblock || BZR_TRAV_BUNDLE, "BZR_TRAV_ABLOCK needs the bundle walk");
     __shared__ float ubl[16];                                  // the block's union bundle (words 0..12)
@@ -1591,11 +1742,12 @@ __global__ __launch_bounds__(kBlk) BZR_TRAV_ATTR void k_traverse(MeshView m, con
 #else
     float4 *arec = nullptr;
 #endif
-    traverse_rays<kBlk, kAblock>(m, rays, ld, off, alive, n, w, counters, b * kBlk + threadIdx.x, stack[threadIdx.x >> 6],
-                                 bundle[threadIdx.x >> 6], wpend, wraw, ubl, akeep, wrk, arec);
+    traverse_rays<kBlk, kAblock, kFast>(m, rays, ld, off, alive, n, w, counters, b * kBlk + threadIdx.x,
+                                        stack[threadIdx.x >> 6], bundle[threadIdx.x >> 6], wpend, wraw, hy, ubl, akeep,
+                                        wrk, arec);
   } else {
-    traverse_rays<kBlk, 0>(m, rays, ld, off, alive, n, w, counters, b * kBlk + threadIdx.x, stack[threadIdx.x >> 6],
-                           bundle[threadIdx.x >> 6], wpend, wraw, nullptr, nullptr, wrk);
+    traverse_rays<kBlk, 0, kFast>(m, rays, ld, off, alive, n, w, counters, b * kBlk + threadIdx.x, stack[threadIdx.x >> 6],
+                                  bundle[threadIdx.x >> 6], wpend, wraw, hy, nullptr, nullptr, wrk);
   }
 }
 
@@ -1662,12 +1814,14 @@ __global__ __launch_bounds__(kBlock) void k_place(uint32_t n, uint32_t nb, Work 
     }
 #pragma unroll
     for (uint32_t k = 0; k < 4u; ++k) {
-      o0[k] = w.offs[b[k]];
-      o1[k] = w.offs[b[k] + 1u];
+      const uint32_t bb = b[k] & ~kCandFollow;  // (an in-wave follow request places no pair: BZR_TRAV_HYBRID)
+      o0[k] = w.offs[bb];
+      o1[k] = w.offs[bb + 1u];
     }
 #pragma unroll
     for (uint32_t k = 0; k < 4u; ++k) {
       if (j0 + k >= cnt) break;
+      if (b[k] & kCandFollow) continue;
       const uint32_t dbase = static_cast<uint32_t>(o0[k] >> 32), dlen = 64u * (static_cast<uint32_t>(o1[k] >> 32) - dbase);
       const uint32_t p = r[k] < dlen ? dbase * 64u + r[k] : sparse0 + static_cast<uint32_t>(o0[k]) + (r[k] - dlen);
       w.pairs[p] = make_uint2(idle ? kNoPair : t | ((j0 + k) << 26), b[k]);
@@ -1963,7 +2117,7 @@ __global__ __launch_bounds__(kBlock) BZR_RESOLVE_ATTR void k_resolve(MeshView m,
     load_pair_ray(w.aos, rays, ld, off, i, s, d);
     float best_t = FLT_MAX;
     uint32_t best_b = 0xFFFFFFFFu;
-#pragma unroll 4
+    // (not unrolled: newton_tail's wave vote in div_heights is a convergent operation)
     for (uint32_t b = lo + threadIdx.x; b < hi; b += kBlock) {
       const float4 *qq = m.planar + 4u * b;
       if (!planar_gate(qq[0], qq[1], qq[2], qq[3], s, d)) continue;
@@ -2049,6 +2203,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_small(const uint32_t *__r
 // (same Newton site, patches in index order).
 struct TraceCtr {  // wave-uniform work counters (kCount)
   uint32_t nodes = 0, leaves = 0, gate_tests = 0, rounds = 0, pairs = 0, follows = 0, segments = 0, ovf = 0;
+  uint32_t rounds_odd = 0, runs_odd = 0;  // odd chain segments (a lens's back surface): passes, pairs + follows
 };
 // BZR_TRACE_PRIO (default 3; 0 = off): wave priority (s_setprio) of k_trace's BVH walk phase, back to 0
 // for the Newton passes.  The walk is a chain of dependent scalar loads with little VALU work; issuing
@@ -2725,8 +2880,15 @@ __global__ __launch_bounds__(kTraceBlock) BZR_TRACE_ATTR void k_trace(LensSet le
     if (!BZR_TRACE_PAIRSYNC && !__any(alive)) break;  // (paired waves both run every segment: same meetings)
     const MeshView &m = lenses.lens[k >> 1];
     unsigned long long best;
+    const uint32_t r0 = ctr.rounds, w0 = ctr.pairs + ctr.follows;
     trace_segment<kMode, kFast, kCount>(m, s, d, alive, best, L, lane, ctr, pflag);
-    if (kCount) ctr.segments += popc64(__ballot(alive));
+    if (kCount) {
+      ctr.segments += popc64(__ballot(alive));
+      if (k & 1u) {  // per-segment lane utilisation: front (even) vs back (odd) surfaces
+        ctr.rounds_odd += ctr.rounds - r0;
+        ctr.runs_odd += ctr.pairs + ctr.follows - w0;
+      }
+    }
     Hit h = no_hit();
     uint32_t patch = 0xFFFFFFFFu;
     if (best != ~0ull) h = winner(L, lane, patch);
@@ -2767,15 +2929,15 @@ __global__ __launch_bounds__(kTraceBlock) BZR_TRACE_ATTR void k_trace(LensSet le
       job.wave_clock[2 * (i >> 6) + 1] = t_end - t_start;
     }
   }
-  if (kCount && lane < 8u) {  // one atomic per counter per wave, spread over kCounterReplicas copies
-    const uint32_t v[8] = {ctr.segments, ctr.pairs, ctr.follows, ctr.ovf, ctr.nodes, ctr.leaves, ctr.gate_tests,
-                           ctr.rounds};
-    const uint32_t id[8] = {BZR_COUNTER_SEGMENTS, BZR_COUNTER_PAIRS, BZR_COUNTER_FOLLOWS, BZR_COUNTER_OVERFLOW_RAYS,
-                            BZR_COUNTER_NODE_VISITS, BZR_COUNTER_LEAF_FETCHES, BZR_COUNTER_GATE_TESTS,
-                            BZR_COUNTER_NEWTON_ROUNDS};
+  if (kCount && lane < 10u) {  // one atomic per counter per wave, spread over kCounterReplicas copies
+    const uint32_t v[10] = {ctr.segments, ctr.pairs, ctr.follows, ctr.ovf, ctr.nodes, ctr.leaves, ctr.gate_tests,
+                            ctr.rounds, ctr.rounds_odd, ctr.runs_odd};
+    const uint32_t id[10] = {BZR_COUNTER_SEGMENTS, BZR_COUNTER_PAIRS, BZR_COUNTER_FOLLOWS, BZR_COUNTER_OVERFLOW_RAYS,
+                             BZR_COUNTER_NODE_VISITS, BZR_COUNTER_LEAF_FETCHES, BZR_COUNTER_GATE_TESTS,
+                             BZR_COUNTER_NEWTON_ROUNDS, BZR_COUNTER_ROUNDS_ODD, BZR_COUNTER_RUNS_ODD};
     uint32_t mine = 0, which = 0;
 #pragma unroll
-    for (uint32_t k = 0; k < 8u; ++k)
+    for (uint32_t k = 0; k < 10u; ++k)
       if (lane == k) {
         mine = v[k];
         which = id[k];
@@ -3033,6 +3195,18 @@ uint32_t resident_blocks(bzr_ctx *ctx, K kernel) {
   return blocks;
 }
 
+// BZR_TRAV_HYBRID's threshold: lanes a leaf's gate must pass for k_traverse to run its Newton pass in the wave
+// (environment BZR_HYBRID_T, 1..64; 0 = list every leaf, round 5's pipeline; read once per process).
+uint32_t hybrid_threshold() {
+  static const uint32_t t = [] {
+    const char *e = std::getenv("BZR_HYBRID_T");
+    if (!e || !*e) return (uint32_t)BZR_HYBRID_T_DEFAULT;
+    const long v = std::strtol(e, nullptr, 10);
+    return (uint32_t)(v < 0 ? 0 : v > 64 ? 64 : v);
+  }();
+  return BZR_TRAV_HYBRID ? t : 0u;
+}
+
 // Workspace of the culled path for chunks of up to `chunk` rays over meshes of up to `nb` patches.
 using SplitIt = hipcub::TransformInputIterator<unsigned long long, BucketSplit, const uint32_t *>;
 bzr_status ensure_work(bzr_ctx *ctx, uint32_t chunk, uint32_t nb, Work &w) {
@@ -3043,7 +3217,8 @@ bzr_status ensure_work(bzr_ctx *ctx, uint32_t chunk, uint32_t nb, Work &w) {
   const size_t cap = (size_t)kMaxCand * chunk;
   const size_t bytes = round256(32) + round256((size_t)(hn + 1) * 4) + round256((size_t)(hn + 1) * 8) + 2 * round256(cap * 4) +
                        round256((size_t)chunk * 4) + round256((size_t)chunk * 8) + round256(kSlotWords * cap * 4) +
-                       round256((cap + 64 * ((size_t)nb + 1)) * 8) + round256(cap * 4) + round256((size_t)chunk * 4) +
+                       round256((cap + 64 * ((size_t)nb + 1) + (BZR_TRAV_HYBRID ? cap : 0)) * 8) + round256(cap * 4) +
+                       round256((size_t)chunk * 4) +
                        (BZR_STAGED_AOS ? round256((size_t)chunk * 32) : 0) + round256(cub_bytes);
   const size_t had = ctx->work_bytes;
   if (bzr_status s = ensure_buffer(ctx->work, ctx->work_bytes, bytes)) return s;
@@ -3057,13 +3232,16 @@ bzr_status ensure_work(bzr_ctx *ctx, uint32_t chunk, uint32_t nb, Work &w) {
   w.count = st.take<uint32_t>(chunk);
   w.key = st.take<unsigned long long>(chunk);
   w.slot = st.take<float>(kSlotWords * cap);
-  w.pairs = st.take<uint2>(cap + 64 * ((size_t)nb + 1));  // dense chunks (< 64 padding slots per patch) + sparse
+  // dense chunks (< 64 padding slots per patch) + sparse; then (BZR_TRAV_HYBRID) the in-wave follow requests' records
+  w.pairs = st.take<uint2>(cap + 64 * ((size_t)nb + 1) + (BZR_TRAV_HYBRID ? cap : 0));
   w.fol = st.take<uint32_t>(cap);
   w.ovf = st.take<uint32_t>(chunk);
   w.aos = BZR_STAGED_AOS ? st.take<float4>((size_t)2 * chunk) : nullptr;
   w.cub = st.take<char>(cub_bytes ? cub_bytes : 1);
   w.cub_bytes = cub_bytes;
   w.cap = static_cast<uint32_t>(cap);
+  w.hbase = static_cast<uint32_t>(cap + 64 * ((size_t)nb + 1));
+  w.hyb_t = hybrid_threshold();
   return BZR_OK;
 }
 
@@ -3076,9 +3254,10 @@ bzr_status ensure_work(bzr_ctx *ctx, uint32_t chunk, uint32_t nb, Work &w) {
 #define BZR_CHUNK_LOG2 23
 #endif
 constexpr uint32_t kChunk = 1u << BZR_CHUNK_LOG2;
-constexpr size_t kWorkBytesPerRay = (size_t)kMaxCand * (4 + 4 + 48 + 8 + 4) + 16 + (BZR_STAGED_AOS ? 32 : 0);
+constexpr size_t kWorkBytesPerRay = (size_t)kMaxCand * (4 + 4 + 48 + 8 + 4 + (BZR_TRAV_HYBRID ? 8 : 0)) + 16 + (BZR_STAGED_AOS ? 32 : 0);
 static_assert(BZR_CHUNK_LOG2 <= 26, "pair records hold a chunk's ray index in 26 bits");
-static_assert((uint64_t)kMaxCand * kChunk + 64ull * (kStagedPatchLimit + 1) < (1ull << 32), "32-bit pair indices");
+static_assert((uint64_t)kMaxCand * kChunk * (BZR_TRAV_HYBRID ? 2 : 1) + 64ull * (kStagedPatchLimit + 1) < (1ull << 32),
+              "32-bit pair indices");
 static_assert(kMaxCand <= 64, "winner keys hold a list slot in 6 bits");
 uint32_t chunk_for(bzr_ctx *ctx, uint64_t n) {
   if (!ctx->chunk_cap) {
@@ -3109,10 +3288,10 @@ bzr_status run_culled(bzr_ctx *ctx, const MeshView &mv, const float *rays, uint3
   ctx->zero_ctr = nullptr;  // valid again only once this segment is fully enqueued
   unsigned long long *const ctr = (ctx->counting && ctx->counters) ? ctx->counters : nullptr;
   if (BZR_TRAV_ABLOCK && mv.n_always > kAblockMin && mv.n_always <= kAblockMax)  // block-level always-list pre-test
-    launch_on(ctx, ctx->stream, dim3(kAblockBlock), BZR_KERNEL_TRAVERSE, k_traverse<kAblockBlock, BZR_TRAV_ABLOCK>,
+    launch_on(ctx, ctx->stream, dim3(kAblockBlock), BZR_KERNEL_TRAVERSE, k_traverse<kAblockBlock, BZR_TRAV_ABLOCK, kFast>,
               dim3((n + kAblockBlock - 1) / kAblockBlock), mv, rays, ld, off, alive, n, w, ctr);
   else
-    launch_on(ctx, ctx->stream, dim3(kTravBlock), BZR_KERNEL_TRAVERSE, k_traverse<kTravBlock, 0>,
+    launch_on(ctx, ctx->stream, dim3(kTravBlock), BZR_KERNEL_TRAVERSE, k_traverse<kTravBlock, 0, kFast>,
               dim3((n + kTravBlock - 1) / kTravBlock), mv, rays, ld, off, alive, n, w, ctr);
   {
     Span sp(ctx, BZR_KERNEL_BUCKET);
@@ -3140,7 +3319,10 @@ bzr_status run_culled(bzr_ctx *ctx, const MeshView &mv, const float *rays, uint3
   if (ctx->counting && ctx->counters)  // before k_finish, which clears the counters
     hipLaunchKernelGGL(k_count, dim3(1), dim3(64), 0, ctx->stream, w, nb, ctx->counters);
   if (kMode == kModeHits && BZR_FINISH_NORAY)  // the overflow rays first (k_finish clears their count)
-    launch(ctx, BZR_KERNEL_FINISH, k_finish_ovf<kFast>, dim3(16), mv, rays, ld, off, w, o);
+    // (grid-stride over the overflow list; sized for the worst case -- every ray of the chunk beyond s_max -- since
+    // the count is only known on the device: blocks past it exit at once)
+    launch(ctx, BZR_KERNEL_FINISH, k_finish_ovf<kFast>, dim3(std::min<uint32_t>(grid_for(n), 512u)), mv, rays, ld, off,
+           w, o);
   launch(ctx, BZR_KERNEL_FINISH, k_finish<kMode, kFast>, dim3(grid_for(n)), mv, rays, ld, off, n, w, o);
   BZR_HIP(hipGetLastError());
   ctx->zero_ctr = w.ctr;  // k_place cleared the histogram, k_finish the counters
@@ -3171,6 +3353,15 @@ bzr_status run_fused(bzr_ctx *ctx, const LensSet &set, const TraceJob &job, uint
       ctx->sched_cap = tiles;
     }
     j.cost = ctx->sched;
+    // the saved order belongs to a call of this size over the same lenses in the same mode (any other
+    // call rebuilds it -- its bits would not change either way, the order is a permutation of whole tiles)
+    uint64_t key = 0xcbf29ce484222325ull ^ (uint64_t)kMode;
+    for (uint32_t l = 0; l < set.count; ++l)
+      key = (key ^ reinterpret_cast<uintptr_t>(set.lens[l].full)) * 0x100000001b3ull;
+    if (ctx->sched_key != key) {
+      ctx->sched_key = key;
+      ctx->sched_waves = 0;
+    }
     if (ctx->sched_waves == tiles) {
       j.order = ctx->sched + ctx->sched_cap;
       ++ctx->sched_calls;
@@ -3853,7 +4044,31 @@ __global__ __launch_bounds__(kBlock) void k_debug_unit(const float *__restrict__
 #pragma unroll
   for (int k = 0; k < 6; ++k) out[(size_t)k * n + i] = r[k];
 }
+// newton_tail's bracket quotients (div_heights) beside one correctly rounded division each.
+__global__ __launch_bounds__(kBlock) void k_debug_div_heights(const float *__restrict__ a, uint32_t n,
+                                                              float *__restrict__ out) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const float hin = a[i], hout = a[(size_t)n + i], ic = a[(size_t)2 * n + i];
+  float din, dout;
+  div_heights(hin, hout, ic, din, dout);
+  out[i] = din;
+  out[(size_t)n + i] = dout;
+  out[(size_t)2 * n + i] = div_rn(hin, ic);
+  out[(size_t)3 * n + i] = div_rn(hout, ic);
+}
 }  // namespace
+
+extern "C" bzr_status bzr_debug_div_heights(void *ctxp, const float *a, uint32_t n, float *out) {
+  bzr_ctx *ctx = static_cast<bzr_ctx *>(ctxp);
+  if (!ctx) return set_error(BZR_ERR_INVALID_ARGUMENT, "null context");
+  if (n == 0) return BZR_OK;
+  if (!a || !out) return set_error(BZR_ERR_INVALID_ARGUMENT, "null buffer");
+  DeviceGuard g(ctx->device);
+  hipLaunchKernelGGL(k_debug_div_heights, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, ctx->stream, a, n, out);
+  BZR_HIP(hipGetLastError());
+  return BZR_OK;
+}
 
 extern "C" bzr_status bzr_debug_wave_clock(void *ctxp, unsigned long long *clock, uint32_t waves) {
   bzr_ctx *ctx = static_cast<bzr_ctx *>(ctxp);

@@ -79,6 +79,18 @@ void traceChain(std::vector<BezierLens const *> const &lenses, Ray const *rays, 
   }
 }
 
+namespace {
+// The contexts' locks, taken in id order: two calls over shared contexts cannot deadlock (a repeated context is
+// locked once).
+std::vector<std::unique_lock<std::mutex>> lock_in_order(std::vector<Context *> order) {
+  std::sort(order.begin(), order.end(), [](Context *a, Context *b) { return a->id() < b->id(); });
+  order.erase(std::unique(order.begin(), order.end()), order.end());
+  std::vector<std::unique_lock<std::mutex>> hold;
+  for (Context *c : order) hold.emplace_back(c->lock());
+  return hold;
+}
+}  // namespace
+
 void traceChainTiled(std::vector<Context *> const &ctxs, std::vector<BezierLens const *> const &lenses,
                      Ray const *rays, std::size_t n, Ray *outRays, RefractionResult *outStatus,
                      uint32_t *outSegments, uint32_t tileRays) {
@@ -90,11 +102,7 @@ void traceChainTiled(std::vector<Context *> const &ctxs, std::vector<BezierLens 
     handles.push_back(c->get());
     for (auto const *l : lenses) meshes.push_back(l->getMesh().device(*c));
   }
-  std::vector<Context *> order(ctxs);  // held in id order: two such calls over shared contexts cannot deadlock
-  std::sort(order.begin(), order.end(), [](Context *a, Context *b) { return a->id() < b->id(); });
-  order.erase(std::unique(order.begin(), order.end()), order.end());  // (a repeated context: bzr_trace_tiled says so)
-  std::vector<std::unique_lock<std::mutex>> hold;
-  for (Context *c : order) hold.emplace_back(c->lock());
+  auto hold = lock_in_order(ctxs);
   if (n > UINT32_MAX) throw std::length_error("traceChainTiled: more than 2^32-1 rays in one call");
   check(bzr_trace_tiled(handles.data(), static_cast<uint32_t>(handles.size()), meshes.data(), ri.data(),
                         static_cast<uint32_t>(lenses.size()), records(rays), static_cast<uint32_t>(n), tileRays,
@@ -110,7 +118,10 @@ TiledChain::TiledChain(std::vector<std::vector<Context *>> const &slots, std::ve
   std::vector<bzr_ctx *> handles;
   for (auto const &slot : slots) {
     if (slot.size() != mDevices) throw std::invalid_argument("TiledChain: every slot lists the same devices");
-    for (Context *c : slot) handles.push_back(c->get());
+    for (Context *c : slot) {
+      handles.push_back(c->get());
+      mContexts.push_back(c);
+    }
   }
   for (auto const *l : lenses) mRi.push_back(l->getRefractiveIndex());
   for (Context *c : slots[0])  // device d's lens copies (meshes are device-scoped: every slot's context on d uses them)
@@ -128,30 +139,38 @@ int TiledChain::transport() const {
 }
 
 void TiledChain::setRays(Ray const *rays) {
+  auto hold = lock_in_order(mContexts);
   check(bzr_tiled_set_rays(mPlan, records(rays), BZR_HOST_PTRS | BZR_RAYS_AOS));
 }
 
 void TiledChain::setRaysDevice(float const *raysSoaOnDevice0) {
+  auto hold = lock_in_order(mContexts);
   check(bzr_tiled_set_rays(mPlan, raysSoaOnDevice0, BZR_DEVICE_PTRS));
 }
 
 void TiledChain::trace(float *outRays, uint32_t *outStatus, uint32_t *outSegments, uint32_t flags) {
+  auto hold = lock_in_order(mContexts);
   check(bzr_tiled_trace(mPlan, mMeshes.data(), mRi.data(), static_cast<uint32_t>(mRi.size()), outRays, outStatus,
                         outSegments, flags | BZR_DEVICE_PTRS));
 }
 
 void TiledChain::trace(Ray *outRays, RefractionResult *outStatus, uint32_t *outSegments, uint32_t flags) {
+  auto hold = lock_in_order(mContexts);
   check(bzr_tiled_trace(mPlan, mMeshes.data(), mRi.data(), static_cast<uint32_t>(mRi.size()), records(outRays),
                         words(outStatus), outSegments, (flags & ~uint32_t(BZR_DEVICE_PTRS)) | BZR_RAYS_AOS));
 }
 
 uint32_t TiledChain::calibrate(uint32_t flags) {
   uint32_t cap = 0;
+  auto hold = lock_in_order(mContexts);
   check(bzr_tiled_calibrate(mPlan, mMeshes.data(), mRi.data(), static_cast<uint32_t>(mRi.size()), flags, &cap));
   return cap;
 }
 
-void TiledChain::sync() { check(bzr_tiled_sync(mPlan)); }
+void TiledChain::sync() {
+  auto hold = lock_in_order(mContexts);
+  check(bzr_tiled_sync(mPlan));
+}
 
 }  // namespace bzr
 

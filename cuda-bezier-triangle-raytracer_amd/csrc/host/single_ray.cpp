@@ -68,6 +68,10 @@ inline f3 unit_or_self(f3 a, float z) {  // Eigen normalized(): a / sqrt(z) when
   const float s = sqrt_rn(z);
   return mk(div_rn(a.x, s), div_rn(a.y, s), div_rn(a.z, s));
 }
+inline void div_heights(float hin, float hout, float ic, float &din, float &dout) {
+  din = div_rn(hin, ic);
+  dout = div_rn(hout, ic);
+}
 #include "../device/patch_math_body.inc"
 }  // namespace exact
 using namespace exact;

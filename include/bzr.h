@@ -175,7 +175,9 @@ enum {
   BZR_COUNTER_LEAF_FETCHES = 6,  /* fused path: leaf gate records fetched (per wave, 64 B each) */
   BZR_COUNTER_GATE_TESTS = 7,    /* fused path: planar gates evaluated (per ray: lanes whose box test hit a fetched leaf) */
   BZR_COUNTER_NEWTON_ROUNDS = 8, /* fused path: patch-uniform Newton passes (per wave; cThis + follow-side) */
-  BZR_COUNTER_COUNT = 9
+  BZR_COUNTER_ROUNDS_ODD = 9,    /* fused path: the passes of odd chain segments (refract(OUTSIDE): a lens's back surface) */
+  BZR_COUNTER_RUNS_ODD = 10,     /* fused path: their Newton runs (pairs + follow retries) */
+  BZR_COUNTER_COUNT = 11
 };
 /* While enabled, each culled segment adds its counts on the device (one tiny kernel per segment). */
 bzr_status bzr_ctx_counters(bzr_ctx *ctx, int32_t enable);

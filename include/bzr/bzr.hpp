@@ -459,6 +459,8 @@ void traceChainTiled(std::vector<Context *> const &ctxs, std::vector<BezierLens 
 // results gathered to device 0 on the device side (RCCL over xGMI between distinct devices, peer copies
 // otherwise).  The device-pointer trace() is asynchronous (frames on different slots overlap; keep one set
 // of outputs per frame in flight, sync() before reading them); the host-pointer trace() is synchronous.
+// Every member takes its contexts' locks (in context id order, as traceChainTiled does), so the contexts may
+// also serve batch calls from other threads.
 class TiledChain {
  public:
   TiledChain(std::vector<std::vector<Context *>> const &slots, std::vector<BezierLens const *> const &lenses,
@@ -466,9 +468,11 @@ class TiledChain {
   ~TiledChain();
   TiledChain(TiledChain const &) = delete;
   TiledChain &operator=(TiledChain const &) = delete;
-  int transport() const;                                  // BZR_GATHER_RCCL or BZR_GATHER_PEER
-  void setRays(Ray const *rays);                          // n host rays, tile-major; stay resident
-  void setRaysDevice(float const *raysSoaOnDevice0);      // [6][n] SoA on slot 0 device 0
+  int transport() const;  // BZR_GATHER_RCCL, BZR_GATHER_PEER, or BZR_GATHER_DIRECT (AUTO's choice for one device)
+  void setRays(Ray const *rays);  // n host rays, tile-major; copied before it returns, then resident
+  // [6][n] SoA on slot 0 device 0: the copy is only queued (on device 0's stream); the source must stay unchanged
+  // and allocated until the next sync()
+  void setRaysDevice(float const *raysSoaOnDevice0);
   void trace(float *outRaysSoa, uint32_t *outStatus, uint32_t *outSegments = nullptr, uint32_t flags = 0);  // device 0
   void trace(Ray *outRays, RefractionResult *outStatus, uint32_t *outSegments = nullptr, uint32_t flags = 0);  // host
   // Compact gather (bzr_tiled_calibrate): one counted frame, then only the refracted rays cross to device 0
@@ -480,6 +484,7 @@ class TiledChain {
   bzr_tiled *mPlan = nullptr;
   std::size_t mDevices = 0, mN = 0;
   std::vector<bzr_mesh const *> mMeshes;  // [device][lens]
+  std::vector<Context *> mContexts;      // every slot's contexts (their locks)
   std::vector<float> mRi;
 };
 }  // namespace bzr

@@ -52,6 +52,10 @@ int32_t bzr_debug_traverse_bundle(const void *patches, uint32_t n, uint32_t stri
  * rounded sqrt and one division per component.  Asynchronous on the context's stream.  ctx is a
  * bzr_ctx* (bzr.h). */
 int32_t bzr_debug_unit(void *ctx, const float *a, uint32_t n, float *out);
+/* Device check of newton_tail's bracket quotients hIn / cos, hOut / cos (patch_math.hpp div_heights: one shared
+ * reciprocal where proven): `a` device memory [3][n] (hIn, hOut, cos), `out` device memory [4][n]: rows 0-1 the
+ * product's quotients, rows 2-3 one correctly rounded division each.  Asynchronous on the context's stream. */
+int32_t bzr_debug_div_heights(void *ctx, const float *a, uint32_t n, float *out);
 /* Per-wave timing of the fused kernel: while set, every fused call (k_trace, one 64-ray wave per 64
  * consecutive rays) of `n` <= 64 * waves rays writes clock[2w] = the wave's start (s_memtime ticks) and
  * clock[2w+1] = its duration, for wave w = ray index / 64.  `clock` is device memory; NULL turns it off.

@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--side", type=int, default=0, help="rays per image side (0 = the config's own)")
     ap.add_argument("--pipeline", default="fused", choices=["fused", "staged", "auto"])
+    ap.add_argument("--wave", default="8x8", help="rows x cols of image pixels per 64-ray wave (ray order)")
     a = ap.parse_args()
     import torch
 
@@ -48,7 +49,8 @@ def main():
     pflag = {"fused": bzr_amd.PIPELINE_FUSED, "staged": bzr_amd.PIPELINE_STAGED, "auto": 0}[a.pipeline]
     patches = [build_lens(bzr_amd.TriMesh, l).bezier_patches() for l in cfg.lenses]
     ris = (ctypes.c_float * len(patches))(*[l.ri for l in cfg.lenses])
-    rays = torch.from_numpy(grid_rays(cfg, side=a.side) if a.side else grid_rays(cfg)).cuda()
+    wave = tuple(int(x) for x in a.wave.split("x"))
+    rays = torch.from_numpy(grid_rays(cfg, side=a.side or None, wave=wave)).cuda()
     n = rays.shape[1]
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
