@@ -45,7 +45,7 @@ PATCH_WORDS = 66  # sizeof(bzr_patch) / 4
 KERNELS = ("k_traverse", "bucket", "k_newton", "k_follow", "k_finish", "k_overflow", "k_intersect_scan",
            "k_refract_scan", "k_chain_scan", "k_patch", "k_newton_lane", "k_trace")  # BZR_KERNEL_* ids
 COUNTERS = ("segments", "pairs", "follows", "overflow_rays", "lane_chunks", "node_visits", "leaf_fetches",
-            "gate_tests", "newton_rounds", "rounds_odd", "runs_odd")  # BZR_COUNTER_* ids
+            "gate_tests", "newton_rounds", "rounds_odd", "runs_odd", "dirty_rows")  # BZR_COUNTER_* ids
 HIT_FIELDS = 13
 
 _P = ctypes.c_void_p

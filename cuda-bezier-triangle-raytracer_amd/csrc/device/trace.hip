@@ -544,8 +544,17 @@ __device__ __forceinline__ void node_children(const bzr_host::Bvh4Node *nodes, c
 //   k_finish    winner -> BezierIntersection / refraction (overflow rays: their winner re-evaluated)
 // For one ray (t order, patch, slot) orders like (t, scanned patch index): the atomicMin winner is the
 // reference's strict-< in-order winner (record()).
+// BZR_ROWS_DIRECT: where the Newton stage writes an intersect segment's hits (RowOut::rows non-null: the caller's
+// hit rows, see record_row) instead of the list slots.
+struct RowOut {
+  float *rows = nullptr;        // [13][ld] hit rows, ray i at off + i
+  uint32_t ld = 0, off = 0;
+  uint32_t *count = nullptr;    // Work::count (kDirty)
+  uint32_t *dirty = nullptr;    // [chunk] rays whose row two improving pairs may have written in either order
+  uint32_t *ndirty = nullptr;   // Work::ctr + 4
+};
 struct Work {
-  uint32_t *ctr;     // [0] follow count, [1] overflow count, [2] rays traced, [3] pairs listed
+  uint32_t *ctr;     // [0] follow count, [1] overflow count, [2] rays traced, [3] pairs listed, [4] dirty rows
   uint32_t *hist;    // [nb + 1] pair counts per patch (hist[nb] = 0); 256 bytes after ctr
   unsigned long long *offs;  // [nb + 1] exclusive prefix of bucket_split(hist); offs[nb] = the totals
   uint32_t *cand;    // [kMaxCand][n]
@@ -557,6 +566,8 @@ struct Work {
                      // region; a follow request adds its side << 30 to the patch word
   uint32_t *fol;     // [cap] follow requests: pair indices
   uint32_t *ovf;     // [n]
+  uint32_t *dirty;   // [n] BZR_ROWS_DIRECT: rays whose hit row k_finish_ovf evaluates again
+  RowOut ro;         // BZR_ROWS_DIRECT (intersect segments): the Newton stage's direct row writes
   float4 *aos;       // [2 * chunk] the chunk's rays as 32-byte records (BZR_STAGED_AOS)
   void *cub;
   size_t cub_bytes;
@@ -645,6 +656,55 @@ __device__ __forceinline__ void record(float *__restrict__ slot, uint32_t n, uin
 #if !BZR_RECORD_RET
   atomicMin(key, k);
 #endif
+}
+
+// BZR_ROWS_DIRECT (A/B knob, default 0): an intersect segment's Newton stage writes a pair's hit straight into the caller's
+// hit rows instead of its 48-byte list slot, and k_finish only writes the misses' rows -- it no longer reads a slot
+// and rewrites every hit row (cfg5: k_finish 822 -> ~260 MB per 8 M-ray chunk).  Ordering: a pair whose key improves
+// the ray's (the returning atomicMin) writes its 13 words write-through (sc1: the line leaves the XCD's L2 for the
+// memory side, MI355X_MICROARCH.md visibility table), waits for them (vmcnt(0)) and reads the key again at the
+// coherence point (a second atomicMin).  Still its own key: any later improvement's atomic comes after that read, so
+// its stores land after these and its row is the final one.  Changed: another pair improved meanwhile and the two
+// writes may have landed in either order, so the ray is marked dirty (kDirty in its count, once, and listed) and
+// k_finish_ovf evaluates its final winner again from the key (patch b, cThis, then the follow side's neighbour with
+// cNone: the sequence that produced the key, same bits).  Misses are written by k_finish, overflow rays by
+// k_finish_ovf, as before.  Measured (profiles/r06_ab_rows_direct.jsonl; all GPU tests bit-identical with it on):
+// 0.43 % of cfg5's rays dirty; lone frames cfg5 -0.3 % (k_finish 1.17 -> 0.64 ms per frame, but k_newton +0.25 and
+// k_resolve +0.13: the drain stalls the VALU-bound waves), cfg3 +3 %; at bench level, frames in flight, cfg5 6 758 ->
+// 6 517 Mrays/s and cfg3 9 695 -> 9 433 -- the write-through stores cost more than k_finish's HBM bytes save.  Checking
+// a row at the lane's next step instead (its stores long done): 3.4x the dirty rows and slower.  Not kept.
+#ifndef BZR_ROWS_DIRECT
+#define BZR_ROWS_DIRECT 0
+#endif
+constexpr uint32_t kDirty = 0x10000u;  // count flag (above kOverflow): the hit row is evaluated again
+__device__ __forceinline__ void store_wt(float *p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+// Record a lane's hit (wr) -- ray `ray`'s list slot j, candidate patch b, from patch src -- into its row.
+__device__ __forceinline__ void row_step(const RowOut &ro, unsigned long long *key, bool wr, uint32_t ray, uint32_t j,
+                                         uint32_t b, const Hit &h, uint32_t src) {
+  wr = wr && h.t < FLT_MAX;
+  const unsigned long long kn = ((unsigned long long)t_order(h.t) << 32) | (b << 6) | j;
+  if (wr) wr = kn < atomicMin(&key[ray], kn);
+  if (!__any(wr)) return;
+  if (wr) {
+    const size_t ld = ro.ld, i = (size_t)ro.off + ray;
+    float *r = ro.rows;
+    store_wt(r + i, h.t);
+    store_wt(r + ld + i, h.point.x);
+    store_wt(r + 2 * ld + i, h.point.y);
+    store_wt(r + 3 * ld + i, h.point.z);
+    store_wt(r + 4 * ld + i, h.cs);
+    store_wt(r + 5 * ld + i, h.bary.x);
+    store_wt(r + 6 * ld + i, h.bary.y);
+    store_wt(r + 7 * ld + i, h.bary.z);
+    store_wt(r + 8 * ld + i, h.normal.x);
+    store_wt(r + 9 * ld + i, h.normal.y);
+    store_wt(r + 10 * ld + i, h.normal.z);
+    store_wt(r + 11 * ld + i, __uint_as_float(kIntersect));
+    store_wt(r + 12 * ld + i, __uint_as_float(src));
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the rows have reached the memory side
+  if (wr && atomicMin(&key[ray], kn) != kn && !(atomicOr(&ro.count[ray], kDirty) & kDirty))
+    ro.dirty[atomicAdd(ro.ndirty, 1u)] = ray;
 }
 
 // Word group g of a 64-byte leaf record (planar record, patch index in the last word): q0..q3 of the gate.
@@ -1866,7 +1926,7 @@ __global__ __launch_bounds__(kBlock) BZR_NEWTON_ATTR void k_newton(const float *
                                                    uint32_t ld, uint32_t off, uint32_t n, float *__restrict__ slot,
                                                    unsigned long long *__restrict__ key,
                                                    uint32_t *__restrict__ fol, uint32_t *__restrict__ nfol,
-                                                   const float4 *__restrict__ aos) {
+                                                   const float4 *__restrict__ aos, RowOut ro) {
   __shared__ uint32_t fbuf[kWaves][kFolBuf];
   const uint32_t wv = threadIdx.x >> 6;
   uint32_t nf = 0;  // staged follow requests of this wave (uniform)
@@ -1908,8 +1968,14 @@ __global__ __launch_bounds__(kBlock) BZR_NEWTON_ATTR void k_newton(const float *
 #endif
     bool is_fol = false;
     const auto pa = uniform_patch(full, b);
-    if (todo) {
+    if (ro.rows) {  // BZR_ROWS_DIRECT
+      Hit h = no_hit();
       // every pair passed this patch's planar gate in k_traverse (same arithmetic, same record values)
+      if (todo) h = patch_intersect<BZR_NEWTON_GATED != 0, kFast>(pa, s, d, false);
+      row_step(ro, key, todo && h.what == kIntersect, ray, j, b, h, b);
+      is_fol = todo && h.what <= kFollow2;
+      if (is_fol) reinterpret_cast<uint32_t *>(pairs)[2u * p + 1u] = b | (h.what << 30);  // the side, for k_resolve
+    } else if (todo) {
       const Hit h = patch_intersect<BZR_NEWTON_GATED != 0, kFast>(pa, s, d, false);
       if (h.what == kIntersect) record(slot, n, ray, j, b, h, b, &key[ray]);
       is_fol = h.what <= kFollow2;
@@ -1935,7 +2001,7 @@ __global__ __launch_bounds__(kBlock) void k_newton_lane(const float *__restrict_
                                                         uint32_t ld, uint32_t off, uint32_t n, float *__restrict__ slot,
                                                         unsigned long long *__restrict__ key,
                                                         uint32_t *__restrict__ fol, uint32_t *__restrict__ nfol,
-                                                        const float4 *__restrict__ aos) {
+                                                        const float4 *__restrict__ aos, RowOut ro) {
   const unsigned long long tot = *total;
   const uint32_t base = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(tot >> 32)) * 64u;
   const uint32_t S = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(tot));
@@ -1944,13 +2010,18 @@ __global__ __launch_bounds__(kBlock) void k_newton_lane(const float *__restrict_
     const uint32_t p = base + c * 64u + lane;
     bool is_fol = false;
     const uint2 pr = c * 64u + lane < S ? pairs[p] : make_uint2(kNoPair, 0u);
-    if (pr.x != kNoPair) {
-      const uint32_t ray = pr.x & kRayMask, j = pr.x >> 26, b = pr.y;
+    const bool todo = pr.x != kNoPair;
+    const uint32_t ray = pr.x & kRayMask, j = pr.x >> 26, b = pr.y;
+    Hit h = no_hit();
+    if (todo) {
       f3 s, d;
       load_pair_ray(aos, rays, ld, off, ray, s, d);
       const Patch pa = load_patch(full + (size_t)rec::kWords * b);
-      const Hit h = patch_intersect<BZR_NEWTON_GATED != 0, kFast>(pa, s, d, false);
-      if (h.what == kIntersect) record(slot, n, ray, j, b, h, b, &key[ray]);
+      h = patch_intersect<BZR_NEWTON_GATED != 0, kFast>(pa, s, d, false);
+    }
+    if (ro.rows) row_step(ro, key, todo && h.what == kIntersect, ray, j, b, h, b);
+    else if (todo && h.what == kIntersect) record(slot, n, ray, j, b, h, b, &key[ray]);
+    if (todo) {
       is_fol = h.what <= kFollow2;
       if (is_fol) reinterpret_cast<uint32_t *>(pairs)[2u * p + 1u] = b | (h.what << 30);
     }
@@ -2001,14 +2072,18 @@ template <int kMode, bool kFast>
 __global__ __launch_bounds__(kBlock) BZR_FINISH_ATTR void k_finish(MeshView m, const float *rays, uint32_t ld, uint32_t off, uint32_t n,
                                                    Work w, Out o) {
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  if (blockIdx.x == 0 && threadIdx.x < 4) w.ctr[threadIdx.x] = 0u;  // last reader of the counters this segment
+  if (blockIdx.x == 0 && threadIdx.x < 5) w.ctr[threadIdx.x] = 0u;  // last reader of the counters this segment
   if (i >= n) return;
   const uint32_t gi = off + i;
   if constexpr (kMode == kModeHits && BZR_FINISH_NORAY) {
     // count and key together (testing the count first would make the key and slot loads wait on it)
     const uint32_t c = w.count[i];
     const unsigned long long k = w.key[i];
-    if (c > kMaxCand) return;  // an overflow ray: k_finish_ovf emitted it
+    if (c > kMaxCand) return;  // an overflow ray or a dirty row (BZR_ROWS_DIRECT): k_finish_ovf emitted it
+    if (w.ro.rows) {  // BZR_ROWS_DIRECT: a hit's row is written already; a miss's here
+      if (k == ~0ull) store_hit(o.hits, ld, gi, no_hit(), 0xFFFFFFFFu);
+      return;
+    }
     Hit h = no_hit();
     uint32_t patch = 0xFFFFFFFFu;
     if (k != ~0ull) {
@@ -2070,6 +2145,17 @@ __global__ __launch_bounds__(kBlock) void k_finish_ovf(MeshView m, const float *
     if (k != ~0ull) h = evaluate_patch<kFast>(m, static_cast<uint32_t>(k), s, d, patch);
     store_hit(o.hits, ld, gi, h, patch);
   }
+  // BZR_ROWS_DIRECT's dirty rows: the final key's pair (candidate b, list slot j) evaluated again -- b with cThis,
+  // then its follow side's neighbour with cNone, as k_newton / k_resolve did
+  const uint32_t D = __builtin_amdgcn_readfirstlane(w.ctr[4]);
+  for (uint32_t q = blockIdx.x * kBlock + threadIdx.x; q < D; q += gridDim.x * kBlock) {
+    const uint32_t i = w.dirty[q], gi = off + i;
+    f3 s, d;
+    load_ray(rays, ld, gi, s, d);
+    uint32_t patch = 0xFFFFFFFFu;
+    const Hit h = evaluate_patch<kFast>(m, static_cast<uint32_t>(w.key[i]) >> 6, s, d, patch);
+    store_hit(o.hits, ld, gi, h, patch);
+  }
 }
 
 // The rays k_traverse could not take: the reference's full in-order scan, split into
@@ -2097,15 +2183,26 @@ template <bool kFast>
 __global__ __launch_bounds__(kBlock) BZR_RESOLVE_ATTR void k_resolve(MeshView m, const float *__restrict__ rays, uint32_t ld,
                                                     uint32_t off, uint32_t n, Work w) {
   const uint32_t F = __builtin_amdgcn_readfirstlane(w.ctr[0]);
-  for (uint32_t q = blockIdx.x * kBlock + threadIdx.x; q < F; q += gridDim.x * kBlock) {
-    const uint2 pr = w.pairs[w.fol[q]];
-    const uint32_t ray = pr.x & kRayMask, j = pr.x >> 26, b = pr.y & ~(3u << 30), what = pr.y >> 30;
-    f3 s, d;
-    load_pair_ray(w.aos, rays, ld, off, ray, s, d);
-    const uint32_t nbr = __float_as_uint(m.full[(size_t)rec::kWords * b + rec::kNeigh + what]);
-    Patch pa = load_patch(m.full + (size_t)rec::kWords * nbr);
-    Hit h = patch_intersect<false, kFast>(pa, s, d, true);
-    if (h.what == kIntersect) record(w.slot, n, ray, j, b, h, nbr, &w.key[ray]);  // ranks at its candidate
+  for (uint32_t q0 = blockIdx.x * kBlock; q0 < F; q0 += gridDim.x * kBlock) {  // (whole waves: row_step votes)
+    const uint32_t q = q0 + threadIdx.x;
+    const bool todo = q < F;
+    uint32_t ray = 0u, j = 0u, b = 0u, nbr = 0u;
+    Hit h = no_hit();
+    if (todo) {
+      const uint2 pr = w.pairs[w.fol[q]];
+      ray = pr.x & kRayMask;
+      j = pr.x >> 26;
+      b = pr.y & ~(3u << 30);
+      const uint32_t what = pr.y >> 30;
+      f3 s, d;
+      load_pair_ray(w.aos, rays, ld, off, ray, s, d);
+      nbr = __float_as_uint(m.full[(size_t)rec::kWords * b + rec::kNeigh + what]);
+      Patch pa = load_patch(m.full + (size_t)rec::kWords * nbr);
+      h = patch_intersect<false, kFast>(pa, s, d, true);
+    }
+    // (a follow result ranks at its candidate b)
+    if (w.ro.rows) row_step(w.ro, w.key, todo && h.what == kIntersect, ray, j, b, h, nbr);
+    else if (todo && h.what == kIntersect) record(w.slot, n, ray, j, b, h, nbr, &w.key[ray]);
   }
   const uint32_t V = __builtin_amdgcn_readfirstlane(w.ctr[1]);
   const uint32_t S = (m.n + kOvfSlice - 1) / kOvfSlice;
@@ -2140,6 +2237,7 @@ __global__ void k_count(Work w, uint32_t nb, unsigned long long *__restrict__ co
   counters[BZR_COUNTER_PAIRS] += w.ctr[3];
   counters[BZR_COUNTER_FOLLOWS] += w.ctr[0];
   counters[BZR_COUNTER_OVERFLOW_RAYS] += w.ctr[1];
+  counters[BZR_COUNTER_DIRTY_ROWS] += w.ctr[4];
   // k_newton_lane's chunks; Newton passes = dense chunks + those
   const unsigned long long tot = w.offs[nb];
   const uint32_t sparse_chunks = (static_cast<uint32_t>(tot) + 63u) / 64u;
@@ -3218,7 +3316,7 @@ bzr_status ensure_work(bzr_ctx *ctx, uint32_t chunk, uint32_t nb, Work &w) {
   const size_t bytes = round256(32) + round256((size_t)(hn + 1) * 4) + round256((size_t)(hn + 1) * 8) + 2 * round256(cap * 4) +
                        round256((size_t)chunk * 4) + round256((size_t)chunk * 8) + round256(kSlotWords * cap * 4) +
                        round256((cap + 64 * ((size_t)nb + 1) + (BZR_TRAV_HYBRID ? cap : 0)) * 8) + round256(cap * 4) +
-                       round256((size_t)chunk * 4) +
+                       2 * round256((size_t)chunk * 4) +
                        (BZR_STAGED_AOS ? round256((size_t)chunk * 32) : 0) + round256(cub_bytes);
   const size_t had = ctx->work_bytes;
   if (bzr_status s = ensure_buffer(ctx->work, ctx->work_bytes, bytes)) return s;
@@ -3236,6 +3334,7 @@ bzr_status ensure_work(bzr_ctx *ctx, uint32_t chunk, uint32_t nb, Work &w) {
   w.pairs = st.take<uint2>(cap + 64 * ((size_t)nb + 1) + (BZR_TRAV_HYBRID ? cap : 0));
   w.fol = st.take<uint32_t>(cap);
   w.ovf = st.take<uint32_t>(chunk);
+  w.dirty = st.take<uint32_t>(chunk);
   w.aos = BZR_STAGED_AOS ? st.take<float4>((size_t)2 * chunk) : nullptr;
   w.cub = st.take<char>(cub_bytes ? cub_bytes : 1);
   w.cub_bytes = cub_bytes;
@@ -3254,7 +3353,7 @@ bzr_status ensure_work(bzr_ctx *ctx, uint32_t chunk, uint32_t nb, Work &w) {
 #define BZR_CHUNK_LOG2 23
 #endif
 constexpr uint32_t kChunk = 1u << BZR_CHUNK_LOG2;
-constexpr size_t kWorkBytesPerRay = (size_t)kMaxCand * (4 + 4 + 48 + 8 + 4 + (BZR_TRAV_HYBRID ? 8 : 0)) + 16 + (BZR_STAGED_AOS ? 32 : 0);
+constexpr size_t kWorkBytesPerRay = (size_t)kMaxCand * (4 + 4 + 48 + 8 + 4 + (BZR_TRAV_HYBRID ? 8 : 0)) + 20 + (BZR_STAGED_AOS ? 32 : 0);
 static_assert(BZR_CHUNK_LOG2 <= 26, "pair records hold a chunk's ray index in 26 bits");
 static_assert((uint64_t)kMaxCand * kChunk * (BZR_TRAV_HYBRID ? 2 : 1) + 64ull * (kStagedPatchLimit + 1) < (1ull << 32),
               "32-bit pair indices");
@@ -3287,6 +3386,10 @@ bzr_status run_culled(bzr_ctx *ctx, const MeshView &mv, const float *rays, uint3
                            ctx->stream));
   ctx->zero_ctr = nullptr;  // valid again only once this segment is fully enqueued
   unsigned long long *const ctr = (ctx->counting && ctx->counters) ? ctx->counters : nullptr;
+  // BZR_ROWS_DIRECT: an intersect segment's Newton stage writes the hit rows itself (record_row)
+  w.ro = RowOut{};
+  if (kMode == kModeHits && BZR_ROWS_DIRECT && BZR_FINISH_NORAY && !BZR_TRAV_HYBRID)
+    w.ro = RowOut{o.hits, ld, off, w.count, w.dirty, w.ctr + 4};
   if (BZR_TRAV_ABLOCK && mv.n_always > kAblockMin && mv.n_always <= kAblockMax)  // block-level always-list pre-test
     launch_on(ctx, ctx->stream, dim3(kAblockBlock), BZR_KERNEL_TRAVERSE, k_traverse<kAblockBlock, BZR_TRAV_ABLOCK, kFast>,
               dim3((n + kAblockBlock - 1) / kAblockBlock), mv, rays, ld, off, alive, n, w, ctr);
@@ -3307,9 +3410,9 @@ bzr_status run_culled(bzr_ctx *ctx, const MeshView &mv, const float *rays, uint3
   const uint32_t gn = std::min<uint32_t>(std::max<uint32_t>((kMaxCand * n + kBlock - 1) / kBlock, 1u),
                                          resident_blocks(ctx, k_newton<kFast>));
   launch(ctx, BZR_KERNEL_NEWTON, k_newton<kFast>, dim3(gn), mv.full, w.offs + hn, w.pairs, rays, ld, off, n, w.slot, w.key,
-         w.fol, w.ctr, (const float4 *)w.aos);
+         w.fol, w.ctr, (const float4 *)w.aos, w.ro);
   launch(ctx, BZR_KERNEL_NEWTON_LANE, k_newton_lane<kFast>, dim3(std::min<uint32_t>(std::max<uint32_t>(n / 1024u, 1u), 1024u)),
-         mv.full, w.offs + hn, w.pairs, rays, ld, off, n, w.slot, w.key, w.fol, w.ctr, (const float4 *)w.aos);
+         mv.full, w.offs + hn, w.pairs, rays, ld, off, n, w.slot, w.key, w.fol, w.ctr, (const float4 *)w.aos, w.ro);
   {  // follow retries + overflow rays (whose keys the Newton stage left untouched: their lists are empty)
     const uint64_t items = (uint64_t)n * ((nb + kOvfSlice - 1) / kOvfSlice);
     const uint32_t grid = std::max(std::min<uint32_t>(grid_for(n / 8 + 1), 1024u),

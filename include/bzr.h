@@ -177,7 +177,8 @@ enum {
   BZR_COUNTER_NEWTON_ROUNDS = 8, /* fused path: patch-uniform Newton passes (per wave; cThis + follow-side) */
   BZR_COUNTER_ROUNDS_ODD = 9,    /* fused path: the passes of odd chain segments (refract(OUTSIDE): a lens's back surface) */
   BZR_COUNTER_RUNS_ODD = 10,     /* fused path: their Newton runs (pairs + follow retries) */
-  BZR_COUNTER_COUNT = 11
+  BZR_COUNTER_DIRTY_ROWS = 11,   /* staged intersect: hit rows two improving pairs wrote concurrently (evaluated again) */
+  BZR_COUNTER_COUNT = 12
 };
 /* While enabled, each culled segment adds its counts on the device (one tiny kernel per segment). */
 bzr_status bzr_ctx_counters(bzr_ctx *ctx, int32_t enable);
