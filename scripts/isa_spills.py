@@ -30,6 +30,7 @@ def main():
     ap.add_argument("asm")
     ap.add_argument("--kernel", default="k_traceILi2ELb0ELb0E")
     ap.add_argument("--min-valu", type=int, default=60)
+    ap.add_argument("--blocks", action="store_true", help="list every heavy block")
     a = ap.parse_args()
     body = kernel_body(open(a.asm).read().splitlines(), a.kernel)
     blocks, cur = [], {"label": "entry", "ins": []}
@@ -58,6 +59,13 @@ def main():
                 "scratch": sum(v for k, v in c.items() if k.startswith("scratch_"))}
     print({"kernel": a.kernel, "whole_kernel": row(tot)})
     print({"newton_blocks": nblocks, **row(newton)})
+    if a.blocks:  # every heavy block: the unrolled Newton iterations are the 170-330-VALU blocks with 3 v_div_fmas
+        for b in blocks:
+            c = Counter(b["ins"])
+            valu = sum(v for k, v in c.items() if k.startswith("v_"))
+            if valu >= a.min_valu or c["v_readlane_b32"] or c["v_writelane_b32"]:
+                print(f'  {b["label"]:>12}  valu {valu:4d}  div_fmas {c["v_div_fmas_f32"]}  sqrt {c["v_sqrt_f32"]}  '
+                      f'readlane {c["v_readlane_b32"]}  writelane {c["v_writelane_b32"]}')
 
 
 if __name__ == "__main__":
