@@ -151,7 +151,10 @@ __device__ __forceinline__ uint32_t deal_blocks(uint32_t b, uint32_t nblocks) {
 #ifndef BZR_TRAV_BLOCK
 #define BZR_TRAV_BLOCK 64
 #endif
-constexpr uint32_t kAblockMin = 64, kAblockMax = 1024, kAblockBlock = 256;
+#ifndef BZR_ABLOCK_BLOCK
+#define BZR_ABLOCK_BLOCK 256
+#endif
+constexpr uint32_t kAblockMin = 64, kAblockMax = 1024, kAblockBlock = BZR_ABLOCK_BLOCK;  // threads per pre-testing block
 // BZR_TRAV_ALDS (A/B knob, default 0): with the block pre-test (BZR_TRAV_ABLOCK 1), the block copies its kept
 // always-listed records (the 96 bytes the per-lane gate reads) into LDS once, so the waves' per-lane gates read
 // them there instead of waiting on one scalar load each (when at most kAldsMax are kept; else as before).
@@ -1968,7 +1971,7 @@ __global__ __launch_bounds__(kBlock) BZR_NEWTON_ATTR void k_newton(const float *
 #endif
     bool is_fol = false;
     const auto pa = uniform_patch(full, b);
-    if (ro.rows) {  // BZR_ROWS_DIRECT
+    if (BZR_ROWS_DIRECT && ro.rows) {  // BZR_ROWS_DIRECT
       Hit h = no_hit();
       // every pair passed this patch's planar gate in k_traverse (same arithmetic, same record values)
       if (todo) h = patch_intersect<BZR_NEWTON_GATED != 0, kFast>(pa, s, d, false);
@@ -2019,7 +2022,7 @@ __global__ __launch_bounds__(kBlock) void k_newton_lane(const float *__restrict_
       const Patch pa = load_patch(full + (size_t)rec::kWords * b);
       h = patch_intersect<BZR_NEWTON_GATED != 0, kFast>(pa, s, d, false);
     }
-    if (ro.rows) row_step(ro, key, todo && h.what == kIntersect, ray, j, b, h, b);
+    if (BZR_ROWS_DIRECT && ro.rows) row_step(ro, key, todo && h.what == kIntersect, ray, j, b, h, b);
     else if (todo && h.what == kIntersect) record(slot, n, ray, j, b, h, b, &key[ray]);
     if (todo) {
       is_fol = h.what <= kFollow2;
@@ -2080,7 +2083,7 @@ __global__ __launch_bounds__(kBlock) BZR_FINISH_ATTR void k_finish(MeshView m, c
     const uint32_t c = w.count[i];
     const unsigned long long k = w.key[i];
     if (c > kMaxCand) return;  // an overflow ray or a dirty row (BZR_ROWS_DIRECT): k_finish_ovf emitted it
-    if (w.ro.rows) {  // BZR_ROWS_DIRECT: a hit's row is written already; a miss's here
+    if (BZR_ROWS_DIRECT && w.ro.rows) {  // BZR_ROWS_DIRECT: a hit's row is written already; a miss's here
       if (k == ~0ull) store_hit(o.hits, ld, gi, no_hit(), 0xFFFFFFFFu);
       return;
     }
@@ -2201,7 +2204,7 @@ __global__ __launch_bounds__(kBlock) BZR_RESOLVE_ATTR void k_resolve(MeshView m,
       h = patch_intersect<false, kFast>(pa, s, d, true);
     }
     // (a follow result ranks at its candidate b)
-    if (w.ro.rows) row_step(w.ro, w.key, todo && h.what == kIntersect, ray, j, b, h, nbr);
+    if (BZR_ROWS_DIRECT && w.ro.rows) row_step(w.ro, w.key, todo && h.what == kIntersect, ray, j, b, h, nbr);
     else if (todo && h.what == kIntersect) record(w.slot, n, ray, j, b, h, nbr, &w.key[ray]);
   }
   const uint32_t V = __builtin_amdgcn_readfirstlane(w.ctr[1]);
