@@ -1633,20 +1633,32 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
   if (counters) {  // rays traced (one atomic per wave: on one address, so only with counters on)
     const unsigned long long traced = __ballot(i < n && (alive == nullptr || alive[off + i] != BZR_RR_NONE));
     if ((threadIdx.x & 63u) == 0 && traced) atomicAdd(&w.ctr[2], (uint32_t)__popcll(traced));
-    // walk work (bzr_ctx_counters node_visits / leaf_fetches / gate_tests), spread over the replicas; the in-wave
-    // Newton passes' pairs and passes (BZR_TRAV_HYBRID)
+    // walk work (bzr_ctx_counters node_visits / leaf_fetches / gate_tests), spread over the replicas
     const uint32_t lane = threadIdx.x & 63u, rep = (i >> 6) % kCounterReplicas;
+#if BZR_TRAV_HYBRID  // and the in-wave Newton passes' pairs and passes
     const uint32_t v = lane == 0u ? c_nodes : lane == 1u ? c_leaves : lane == 2u ? c_gates : lane == 3u ? h_pairs : h_rounds;
     const uint32_t which = lane == 0u ? BZR_COUNTER_NODE_VISITS : lane == 1u ? BZR_COUNTER_LEAF_FETCHES
                            : lane == 2u ? BZR_COUNTER_GATE_TESTS : lane == 3u ? BZR_COUNTER_PAIRS : BZR_COUNTER_NEWTON_ROUNDS;
     if (!BZR_TRAV_PHASES && lane < 5u && v) atomicAdd(&counters[(size_t)rep * BZR_COUNTER_COUNT + which], (unsigned long long)v);
+#else
+    (void)h_pairs;
+    (void)h_rounds;
+    const uint32_t v = lane == 0u ? c_nodes : (lane == 1u ? c_leaves : c_gates);
+    const uint32_t which = lane == 0u ? BZR_COUNTER_NODE_VISITS : (lane == 1u ? BZR_COUNTER_LEAF_FETCHES : BZR_COUNTER_GATE_TESTS);
+    if (!BZR_TRAV_PHASES && lane < 3u && v) atomicAdd(&counters[(size_t)rep * BZR_COUNTER_COUNT + which], (unsigned long long)v);
+#endif
   }
 #if BZR_RANK_EARLY == 1
   rank_flush(rpend, w, n, i, cnt);
 #endif
   if (i >= n) return;
   w.count[i] = cnt;
+#if BZR_TRAV_HYBRID
   w.key[i] = cnt > kMaxCand ? ~0ull : hbest;
+#else
+  (void)hbest;
+  w.key[i] = ~0ull;
+#endif
   if (cnt > kMaxCand) w.ovf[atomicAdd(&w.ctr[1], 1u)] = i;
 #if BZR_RANK_EARLY == 3
   const uint32_t lane = threadIdx.x & 63u;
@@ -1691,10 +1703,12 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
   for (uint32_t j0 = 0; __any(j0 < listed); j0 += kRankBatch) {
     uint32_t b[kRankBatch], leader[kRankBatch], below[kRankBatch], base[kRankBatch];
 #pragma unroll
-    for (int k = 0; k < kRankBatch; ++k) b[k] = j0 + k < listed ? w.cand[(size_t)(j0 + k) * n + i] : kCandFollow;
+    for (int k = 0; k < kRankBatch; ++k)
+      b[k] = j0 + k < listed ? w.cand[(size_t)(j0 + k) * n + i] : (BZR_TRAV_HYBRID ? kCandFollow : 0u);
 #pragma unroll
     for (int k = 0; k < kRankBatch; ++k) {
-      const bool pend = !(b[k] & kCandFollow);  // (an in-wave follow request is no pair: BZR_TRAV_HYBRID)
+      // (an in-wave follow request is no pair: BZR_TRAV_HYBRID)
+      const bool pend = BZR_TRAV_HYBRID ? !(b[k] & kCandFollow) : j0 + k < listed;
       unsigned long long group = 0ull;
       bool todo = pend;
       for (;;) {
@@ -1716,7 +1730,7 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
 #pragma unroll
     for (int k = 0; k < kRankBatch; ++k) {
       const uint32_t bs = __shfl(base[k], (int)leader[k], 64);
-      if (!(b[k] & kCandFollow)) w.rank[(size_t)(j0 + k) * n + i] = bs + below[k];
+      if (BZR_TRAV_HYBRID ? !(b[k] & kCandFollow) : j0 + k < listed) w.rank[(size_t)(j0 + k) * n + i] = bs + below[k];
     }
   }
 #else
@@ -1877,14 +1891,16 @@ __global__ __launch_bounds__(kBlock) void k_place(uint32_t n, uint32_t nb, Work 
     }
 #pragma unroll
     for (uint32_t k = 0; k < 4u; ++k) {
-      const uint32_t bb = b[k] & ~kCandFollow;  // (an in-wave follow request places no pair: BZR_TRAV_HYBRID)
+      const uint32_t bb = BZR_TRAV_HYBRID ? b[k] & ~kCandFollow : b[k];  // (BZR_TRAV_HYBRID: follow requests place no pair)
       o0[k] = w.offs[bb];
       o1[k] = w.offs[bb + 1u];
     }
 #pragma unroll
     for (uint32_t k = 0; k < 4u; ++k) {
       if (j0 + k >= cnt) break;
+#if BZR_TRAV_HYBRID
       if (b[k] & kCandFollow) continue;
+#endif
       const uint32_t dbase = static_cast<uint32_t>(o0[k] >> 32), dlen = 64u * (static_cast<uint32_t>(o1[k] >> 32) - dbase);
       const uint32_t p = r[k] < dlen ? dbase * 64u + r[k] : sparse0 + static_cast<uint32_t>(o0[k]) + (r[k] - dlen);
       w.pairs[p] = make_uint2(idle ? kNoPair : t | ((j0 + k) << 26), b[k]);
@@ -1971,14 +1987,19 @@ __global__ __launch_bounds__(kBlock) BZR_NEWTON_ATTR void k_newton(const float *
 #endif
     bool is_fol = false;
     const auto pa = uniform_patch(full, b);
-    if (BZR_ROWS_DIRECT && ro.rows) {  // BZR_ROWS_DIRECT
+#if BZR_ROWS_DIRECT
+    if (ro.rows) {
       Hit h = no_hit();
       // every pair passed this patch's planar gate in k_traverse (same arithmetic, same record values)
       if (todo) h = patch_intersect<BZR_NEWTON_GATED != 0, kFast>(pa, s, d, false);
       row_step(ro, key, todo && h.what == kIntersect, ray, j, b, h, b);
       is_fol = todo && h.what <= kFollow2;
       if (is_fol) reinterpret_cast<uint32_t *>(pairs)[2u * p + 1u] = b | (h.what << 30);  // the side, for k_resolve
-    } else if (todo) {
+    } else
+#else
+    (void)ro;
+#endif
+    if (todo) {
       const Hit h = patch_intersect<BZR_NEWTON_GATED != 0, kFast>(pa, s, d, false);
       if (h.what == kIntersect) record(slot, n, ray, j, b, h, b, &key[ray]);
       is_fol = h.what <= kFollow2;
@@ -2013,6 +2034,7 @@ __global__ __launch_bounds__(kBlock) void k_newton_lane(const float *__restrict_
     const uint32_t p = base + c * 64u + lane;
     bool is_fol = false;
     const uint2 pr = c * 64u + lane < S ? pairs[p] : make_uint2(kNoPair, 0u);
+#if BZR_ROWS_DIRECT
     const bool todo = pr.x != kNoPair;
     const uint32_t ray = pr.x & kRayMask, j = pr.x >> 26, b = pr.y;
     Hit h = no_hit();
@@ -2022,12 +2044,25 @@ __global__ __launch_bounds__(kBlock) void k_newton_lane(const float *__restrict_
       const Patch pa = load_patch(full + (size_t)rec::kWords * b);
       h = patch_intersect<BZR_NEWTON_GATED != 0, kFast>(pa, s, d, false);
     }
-    if (BZR_ROWS_DIRECT && ro.rows) row_step(ro, key, todo && h.what == kIntersect, ray, j, b, h, b);
+    if (ro.rows) row_step(ro, key, todo && h.what == kIntersect, ray, j, b, h, b);
     else if (todo && h.what == kIntersect) record(slot, n, ray, j, b, h, b, &key[ray]);
     if (todo) {
       is_fol = h.what <= kFollow2;
       if (is_fol) reinterpret_cast<uint32_t *>(pairs)[2u * p + 1u] = b | (h.what << 30);
     }
+#else
+    (void)ro;
+    if (pr.x != kNoPair) {
+      const uint32_t ray = pr.x & kRayMask, j = pr.x >> 26, b = pr.y;
+      f3 s, d;
+      load_pair_ray(aos, rays, ld, off, ray, s, d);
+      const Patch pa = load_patch(full + (size_t)rec::kWords * b);
+      const Hit h = patch_intersect<BZR_NEWTON_GATED != 0, kFast>(pa, s, d, false);
+      if (h.what == kIntersect) record(slot, n, ray, j, b, h, b, &key[ray]);
+      is_fol = h.what <= kFollow2;
+      if (is_fol) reinterpret_cast<uint32_t *>(pairs)[2u * p + 1u] = b | (h.what << 30);
+    }
+#endif
     const unsigned long long fm = __ballot(is_fol);
     if (fm) {
       uint32_t fb = 0;
@@ -2148,6 +2183,7 @@ __global__ __launch_bounds__(kBlock) void k_finish_ovf(MeshView m, const float *
     if (k != ~0ull) h = evaluate_patch<kFast>(m, static_cast<uint32_t>(k), s, d, patch);
     store_hit(o.hits, ld, gi, h, patch);
   }
+#if BZR_ROWS_DIRECT
   // BZR_ROWS_DIRECT's dirty rows: the final key's pair (candidate b, list slot j) evaluated again -- b with cThis,
   // then its follow side's neighbour with cNone, as k_newton / k_resolve did
   const uint32_t D = __builtin_amdgcn_readfirstlane(w.ctr[4]);
@@ -2159,6 +2195,7 @@ __global__ __launch_bounds__(kBlock) void k_finish_ovf(MeshView m, const float *
     const Hit h = evaluate_patch<kFast>(m, static_cast<uint32_t>(w.key[i]) >> 6, s, d, patch);
     store_hit(o.hits, ld, gi, h, patch);
   }
+#endif
 }
 
 // The rays k_traverse could not take: the reference's full in-order scan, split into
@@ -2186,6 +2223,7 @@ template <bool kFast>
 __global__ __launch_bounds__(kBlock) BZR_RESOLVE_ATTR void k_resolve(MeshView m, const float *__restrict__ rays, uint32_t ld,
                                                     uint32_t off, uint32_t n, Work w) {
   const uint32_t F = __builtin_amdgcn_readfirstlane(w.ctr[0]);
+#if BZR_ROWS_DIRECT
   for (uint32_t q0 = blockIdx.x * kBlock; q0 < F; q0 += gridDim.x * kBlock) {  // (whole waves: row_step votes)
     const uint32_t q = q0 + threadIdx.x;
     const bool todo = q < F;
@@ -2204,9 +2242,21 @@ __global__ __launch_bounds__(kBlock) BZR_RESOLVE_ATTR void k_resolve(MeshView m,
       h = patch_intersect<false, kFast>(pa, s, d, true);
     }
     // (a follow result ranks at its candidate b)
-    if (BZR_ROWS_DIRECT && w.ro.rows) row_step(w.ro, w.key, todo && h.what == kIntersect, ray, j, b, h, nbr);
+    if (w.ro.rows) row_step(w.ro, w.key, todo && h.what == kIntersect, ray, j, b, h, nbr);
     else if (todo && h.what == kIntersect) record(w.slot, n, ray, j, b, h, nbr, &w.key[ray]);
   }
+#else
+  for (uint32_t q = blockIdx.x * kBlock + threadIdx.x; q < F; q += gridDim.x * kBlock) {
+    const uint2 pr = w.pairs[w.fol[q]];
+    const uint32_t ray = pr.x & kRayMask, j = pr.x >> 26, b = pr.y & ~(3u << 30), what = pr.y >> 30;
+    f3 s, d;
+    load_pair_ray(w.aos, rays, ld, off, ray, s, d);
+    const uint32_t nbr = __float_as_uint(m.full[(size_t)rec::kWords * b + rec::kNeigh + what]);
+    Patch pa = load_patch(m.full + (size_t)rec::kWords * nbr);
+    Hit h = patch_intersect<false, kFast>(pa, s, d, true);
+    if (h.what == kIntersect) record(w.slot, n, ray, j, b, h, nbr, &w.key[ray]);  // ranks at its candidate
+  }
+#endif
   const uint32_t V = __builtin_amdgcn_readfirstlane(w.ctr[1]);
   const uint32_t S = (m.n + kOvfSlice - 1) / kOvfSlice;
   const uint64_t items = (uint64_t)V * S;  // 64-bit: 2^20-ray chunks x slices of meshes above ~8M patches
@@ -3425,9 +3475,10 @@ bzr_status run_culled(bzr_ctx *ctx, const MeshView &mv, const float *rays, uint3
   if (ctx->counting && ctx->counters)  // before k_finish, which clears the counters
     hipLaunchKernelGGL(k_count, dim3(1), dim3(64), 0, ctx->stream, w, nb, ctx->counters);
   if (kMode == kModeHits && BZR_FINISH_NORAY)  // the overflow rays first (k_finish clears their count)
-    // (grid-stride over the overflow list; sized for the worst case -- every ray of the chunk beyond s_max -- since
-    // the count is only known on the device: blocks past it exit at once)
-    launch(ctx, BZR_KERNEL_FINISH, k_finish_ovf<kFast>, dim3(std::min<uint32_t>(grid_for(n), 512u)), mv, rays, ld, off,
+    // (grid-stride over the overflow list, whose length only the device knows.  64 blocks: a batch whose rays all
+    // lie beyond s_max re-evaluates them 16 K at a time, while k_resolve's full scan of the same rays costs a gate per
+    // ray and patch; 512 blocks cost cfg3 frames ~1 % in launch for nothing on the bench configs)
+    launch(ctx, BZR_KERNEL_FINISH, k_finish_ovf<kFast>, dim3(std::min<uint32_t>(grid_for(n), 64u)), mv, rays, ld, off,
            w, o);
   launch(ctx, BZR_KERNEL_FINISH, k_finish<kMode, kFast>, dim3(grid_for(n)), mv, rays, ld, off, n, w, o);
   BZR_HIP(hipGetLastError());

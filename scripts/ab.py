@@ -24,6 +24,8 @@ def bind(path):
     import bzr_amd
     h = ctypes.CDLL(str(path))
     for name, args in bzr_amd._SIGS.items():
+        if not hasattr(h, name):  # (an older build, e.g. a previous round's library: its debug hooks differ)
+            continue
         f = getattr(h, name)
         f.argtypes = args
         f.restype = bzr_amd._RET.get(name, ctypes.c_int32)
