@@ -145,6 +145,9 @@ __device__ __forceinline__ uint32_t deal_blocks(uint32_t b, uint32_t nblocks) {
 // one (compacted) round; 0: off.  A dropped patch is one no ray of the block (so of the wave) can pass: the
 // candidates are unchanged.  cfg5 (131 always-listed patches): k_traverse 4.01 -> 3.84 ms per frame with 1,
 // 4.05 with 2 (profiles/r05_ab_traverse_ablock.jsonl).
+// 3 (A/B): the pre-test in a kernel of its own before k_traverse (k_always_mask: the same union bundle per 256 rays
+// and the same ballots, to a global mask), and k_traverse in one-wave blocks reading its 256-ray block's mask -- no
+// barriers in the walk kernel.
 #ifndef BZR_TRAV_ABLOCK
 #define BZR_TRAV_ABLOCK 1
 #endif
@@ -155,6 +158,7 @@ __device__ __forceinline__ uint32_t deal_blocks(uint32_t b, uint32_t nblocks) {
 #define BZR_ABLOCK_BLOCK 256
 #endif
 constexpr uint32_t kAblockMin = 64, kAblockMax = 1024, kAblockBlock = BZR_ABLOCK_BLOCK;  // threads per pre-testing block
+constexpr uint32_t kAmaskWords = kAblockMax / 64u;  // mask words per pre-testing block (BZR_TRAV_ABLOCK 3)
 // BZR_TRAV_ALDS (A/B knob, default 0): with the block pre-test (BZR_TRAV_ABLOCK 1), the block copies its kept
 // always-listed records (the 96 bytes the per-lane gate reads) into LDS once, so the waves' per-lane gates read
 // them there instead of waiting on one scalar load each (when at most kAldsMax are kept; else as before).
@@ -570,6 +574,7 @@ struct Work {
   uint32_t *fol;     // [cap] follow requests: pair indices
   uint32_t *ovf;     // [n]
   uint32_t *dirty;   // [n] BZR_ROWS_DIRECT: rays whose hit row k_finish_ovf evaluates again
+  unsigned long long *amask;  // BZR_TRAV_ABLOCK 3: [n / 256][kAmaskWords] always-listed patches kept per 256 rays
   RowOut ro;         // BZR_ROWS_DIRECT (intersect segments): the Newton stage's direct row writes
   float4 *aos;       // [2 * chunk] the chunk's rays as 32-byte records (BZR_STAGED_AOS)
   void *cub;
@@ -1303,8 +1308,9 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
 #if BZR_TRAV_PRETEST
   uint32_t nraw = 0;  // leaves queued in raw, not yet pre-tested
 #endif
-  // the always list's block pre-test (every thread of the block gets here: no early exit above)
-  if constexpr (kAblock != 0) {
+  // the always list's block pre-test (every thread of the block gets here: no early exit above); with
+  // BZR_TRAV_ABLOCK 3 k_always_mask did it and akeep points at this ray block's mask
+  if constexpr (kAblock == 1 || kAblock == 2) {
     if (!walk) bundle_setup_dpp(active, s, d, bl, threadIdx.x & 63u);  // (an empty wave's bundle is the identity)
     __syncthreads();
     if (threadIdx.x < 13u) {  // the union over the block's waves with rays (bl - wave * kBundleWords: wave 0's)
@@ -1810,7 +1816,11 @@ __global__ __launch_bounds__(kBlk) BZR_TRAV_ATTR void k_traverse(MeshView m, con
   hy.g = hyb_g[threadIdx.x >> 6];
   hy.t = w.hyb_t;
 #endif
-  if constexpr (kAblock != 0) {
+  if constexpr (kAblock == 3) {  // the mask of this wave's 256-ray block (k_always_mask)
+    traverse_rays<kBlk, 3, kFast>(m, rays, ld, off, alive, n, w, counters, b * kBlk + threadIdx.x, stack[threadIdx.x >> 6],
+                                  bundle[threadIdx.x >> 6], wpend, wraw, hy, nullptr,
+                                  w.amask + (size_t)((b * kBlk) / kAblockBlock) * kAmaskWords, wrk);
+  } else if constexpr (kAblock != 0) {
     static_assert(!kAblock || BZR_TRAV_BUNDLE, "BZR_TRAV_ABLOCK needs the bundle walk");
     __shared__ float ubl[16];                                  // the block's union bundle (words 0..12)
     __shared__ unsigned long long akeep[kAblockMax / 64u];     // block-kept always-listed patches
@@ -1828,6 +1838,42 @@ __global__ __launch_bounds__(kBlk) BZR_TRAV_ATTR void k_traverse(MeshView m, con
   }
 }
 
+
+// BZR_TRAV_ABLOCK 3: the always list's block pre-test as a kernel of its own.  Block b (kAblockBlock rays) forms
+// its waves' ray bundles (bundle_setup_dpp) and their union, ballots always_bundle_keep for every always-listed
+// patch and writes the kept mask to amask[b].  The union is over every ray of the block that is traced (a superset
+// of the walk's active rays: rays beyond s_max take the full scan there), so a dropped patch is one no traced ray of
+// the block can pass -- the candidates are unchanged.
+__global__ __launch_bounds__(kAblockBlock) void k_always_mask(MeshView m, const float *__restrict__ rays, uint32_t ld,
+                                                              uint32_t off, const uint32_t *__restrict__ alive, uint32_t n,
+                                                              unsigned long long *__restrict__ amask) {
+  __shared__ float bundle[kAblockBlock / 64][kBundleWords];
+  __shared__ float ubl[16];
+  const uint32_t i = blockIdx.x * kAblockBlock + threadIdx.x, lane = threadIdx.x & 63u;
+  const bool active = i < n && (alive == nullptr || alive[off + i] != BZR_RR_NONE);
+  f3 s = mk(0.0f, 0.0f, 0.0f), d = s;
+  if (i < n) load_ray(rays, ld, off + i, s, d);
+  bundle_setup_dpp(active, s, d, bundle[threadIdx.x >> 6], lane);
+  __syncthreads();
+  if (threadIdx.x < 13u) {  // the union over the block's waves with rays (as traverse_rays' block pre-test)
+    const uint32_t k = threadIdx.x;
+    float v = k < 12u ? ((k % 6u) < 3u ? __builtin_inff() : -__builtin_inff()) : 1.0f;
+    bool any = false;
+    for (uint32_t q = 0; q < kAblockBlock / 64u; ++q) {
+      const float *bq = bundle[q];
+      if (!(bq[0] <= bq[3])) continue;  // no traced ray in wave q
+      any = true;
+      const float x = bq[k];
+      v = k == 12u ? fminf(v, x) : ((k % 6u) < 3u ? fminf(v, x) : fmaxf(v, x));
+    }
+    ubl[k] = (k == 12u && !any) ? 0.0f : v;
+  }
+  __syncthreads();
+  for (uint32_t base = 0; base < m.n_always; base += kAblockBlock) {
+    const unsigned long long km = __ballot(always_bundle_keep(m.always, base + threadIdx.x, m.n_always, ubl));
+    if (lane == 0u) amask[(size_t)blockIdx.x * kAmaskWords + ((base + threadIdx.x) >> 6)] = km;
+  }
+}
 
 // A bucket of c pairs in the staged layout (BZR_DENSE_MIN): (dense chunks << 32) | pairs in the sparse region.
 struct BucketSplit {
@@ -3369,7 +3415,7 @@ bzr_status ensure_work(bzr_ctx *ctx, uint32_t chunk, uint32_t nb, Work &w) {
   const size_t bytes = round256(32) + round256((size_t)(hn + 1) * 4) + round256((size_t)(hn + 1) * 8) + 2 * round256(cap * 4) +
                        round256((size_t)chunk * 4) + round256((size_t)chunk * 8) + round256(kSlotWords * cap * 4) +
                        round256((cap + 64 * ((size_t)nb + 1) + (BZR_TRAV_HYBRID ? cap : 0)) * 8) + round256(cap * 4) +
-                       2 * round256((size_t)chunk * 4) +
+                       2 * round256((size_t)chunk * 4) + round256(((size_t)chunk + kAblockBlock - 1) / kAblockBlock * kAmaskWords * 8) +
                        (BZR_STAGED_AOS ? round256((size_t)chunk * 32) : 0) + round256(cub_bytes);
   const size_t had = ctx->work_bytes;
   if (bzr_status s = ensure_buffer(ctx->work, ctx->work_bytes, bytes)) return s;
@@ -3388,6 +3434,7 @@ bzr_status ensure_work(bzr_ctx *ctx, uint32_t chunk, uint32_t nb, Work &w) {
   w.fol = st.take<uint32_t>(cap);
   w.ovf = st.take<uint32_t>(chunk);
   w.dirty = st.take<uint32_t>(chunk);
+  w.amask = st.take<unsigned long long>(((size_t)chunk + kAblockBlock - 1) / kAblockBlock * kAmaskWords);
   w.aos = BZR_STAGED_AOS ? st.take<float4>((size_t)2 * chunk) : nullptr;
   w.cub = st.take<char>(cub_bytes ? cub_bytes : 1);
   w.cub_bytes = cub_bytes;
@@ -3443,8 +3490,14 @@ bzr_status run_culled(bzr_ctx *ctx, const MeshView &mv, const float *rays, uint3
   w.ro = RowOut{};
   if (kMode == kModeHits && BZR_ROWS_DIRECT && BZR_FINISH_NORAY && !BZR_TRAV_HYBRID)
     w.ro = RowOut{o.hits, ld, off, w.count, w.dirty, w.ctr + 4};
-  if (BZR_TRAV_ABLOCK && mv.n_always > kAblockMin && mv.n_always <= kAblockMax)  // block-level always-list pre-test
-    launch_on(ctx, ctx->stream, dim3(kAblockBlock), BZR_KERNEL_TRAVERSE, k_traverse<kAblockBlock, BZR_TRAV_ABLOCK, kFast>,
+  if (BZR_TRAV_ABLOCK == 3 && mv.n_always > kAblockMin && mv.n_always <= kAblockMax) {  // pre-test kernel, then the walk
+    Span sp(ctx, BZR_KERNEL_TRAVERSE);
+    hipLaunchKernelGGL(k_always_mask, dim3((n + kAblockBlock - 1) / kAblockBlock), dim3(kAblockBlock), 0, ctx->stream, mv,
+                       rays, ld, off, alive, n, w.amask);
+    hipLaunchKernelGGL((k_traverse<kTravBlock, 3, kFast>), dim3((n + kTravBlock - 1) / kTravBlock), dim3(kTravBlock), 0,
+                       ctx->stream, mv, rays, ld, off, alive, n, w, ctr);
+  } else if (BZR_TRAV_ABLOCK && mv.n_always > kAblockMin && mv.n_always <= kAblockMax)  // block-level always-list pre-test
+    launch_on(ctx, ctx->stream, dim3(kAblockBlock), BZR_KERNEL_TRAVERSE, k_traverse<kAblockBlock, BZR_TRAV_ABLOCK == 3 ? 1 : BZR_TRAV_ABLOCK, kFast>,
               dim3((n + kAblockBlock - 1) / kAblockBlock), mv, rays, ld, off, alive, n, w, ctr);
   else
     launch_on(ctx, ctx->stream, dim3(kTravBlock), BZR_KERNEL_TRAVERSE, k_traverse<kTravBlock, 0, kFast>,

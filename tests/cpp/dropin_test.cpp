@@ -332,6 +332,34 @@ static void hot_path(Mesh const &lensMesh) {
       CHECK(std::memcmp(o.data(), out.data(), out.size() * sizeof(Ray)) == 0);
     }
   }
+  // one context: the DIRECT plan (AUTO's choice for one device), while another thread runs batch chains on the
+  // same context (every TiledChain member takes its contexts' locks, as the batch calls do)
+  {
+    bzr::Context sd(0);
+    bzr::TiledChain one({{&sd}}, {&lens}, n, 512);
+    CHECK(one.transport() == BZR_GATHER_DIRECT);
+    one.setRays(rays.data());
+    std::atomic<int> side_ok{0};
+    std::thread side([&] {
+      for (int k = 0; k < 3; ++k) {
+        std::vector<Ray> o(n);
+        std::vector<RefractionResult> so(n);
+        std::vector<uint32_t> sg(n);
+        bzr::traceChain({&lens}, rays.data(), n, o.data(), so.data(), sg.data(), &sd);
+        side_ok += (so == status && sg == seg && std::memcmp(o.data(), out.data(), n * sizeof(Ray)) == 0) ? 1 : 0;
+      }
+    });
+    for (int k = 0; k < 3; ++k) {
+      std::vector<Ray> o(n);
+      std::vector<RefractionResult> so(n);
+      std::vector<uint32_t> sg(n);
+      one.trace(o.data(), so.data(), sg.data());
+      CHECK(so == status && sg == seg);
+      CHECK(std::memcmp(o.data(), out.data(), out.size() * sizeof(Ray)) == 0);
+    }
+    side.join();
+    CHECK(side_ok == 3);
+  }
   // per-call latency of one ray: host single-ray methods vs the GPU batch of one (launch + PCIe + sync)
   const int calls = 200;
   BezierIntersection sink;
