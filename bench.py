@@ -28,8 +28,9 @@ starts the N rank processes itself (bzr_amd/launch.py: children with RANK / LOCA
 127.0.0.1 rendezvous; the parent touches no GPU and exits with the ranks' status).  Under an external
 launcher (torch.distributed.run) WORLD_SIZE must equal N, else bench.py exits with status 2.  The line
 reports the process group's own world size, the RCCL version and each rank's tile count.
---inflight F (default 3 for the fused pipeline, 2 otherwise): frame k runs on slot k % F (its own context, stream and output buffers), so
-the next frame's waves fill the GPU while a frame's slowest waves finish; every frame is traced in full.
+--inflight F (default: 6 for a rank frame of at most 4 M primaries, else 3 for the fused pipeline and 2 for the
+staged one): frame k runs on slot k % F (its own context, stream and output buffers), so the next frames' waves
+fill the GPU while a frame's slowest waves finish; every frame is traced in full.
 
 Prints ONE JSON line on rank 0; fields are described in DESIGN.md (d).
 """
@@ -96,6 +97,25 @@ BYTES_CHAIN = 24 + 32         # per primary: ray in; ray + status + segment coun
 BYTES_INTERSECT = 24 + 52     # per ray: ray in; BezierIntersection (13 words) out
 
 
+SMALL_FRAME_RAYS = 1 << 22   # a rank's frame at or below this many primaries gets SMALL_FRAME_INFLIGHT slots
+SMALL_FRAME_INFLIGHT = 6
+
+
+def default_inflight(a, world: int) -> int:
+    """--inflight 0: frames in flight from the rank's frame size and the pipeline.  Small frames
+    (cfg2 1024², cfg3 2048², the strong-scaling shares of cfg4 from N = 4) end in short kernels and tails that
+    further frames fill: 6 slots measured +3 % on cfg2 fused and +8 % on cfg3 staged against 3 / 2, and the same
+    on cfg4's N = 4 and N = 8 shares (`profiles/r06_inflight_sweep.jsonl`).  Large frames keep 3 (fused) / 2
+    (staged): cfg4 4096² measures the same at 3 and 6, and the staged pipeline's multi-chunk frames contend
+    beyond two (cfg5 2 against 3, 4, 6)."""
+    from bzr_amd.configs import CONFIGS
+    side = a.side or CONFIGS[a.config].side
+    rays = side * side if a.scaling == "weak" else side * side // max(world, 1)
+    if rays <= SMALL_FRAME_RAYS:
+        return SMALL_FRAME_INFLIGHT
+    return 3 if (a.accel == "bvh" and a.pipeline == "fused") else 2
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -117,7 +137,8 @@ def parse():
                         "kernel per frame (default), staged = the multi-kernel path, auto = the library's choice")
     p.add_argument("--inflight", type=int, default=0,
                    help="frames in flight (each on its own context, stream and output buffers); "
-                        "0 = 3 for the fused pipeline, 2 otherwise (scripts/config_sweep.sh)")
+                        "0 = 6 for a rank frame of at most 4 M primaries, else 3 for the fused pipeline and 2 "
+                        "for the staged one (scripts/inflight_sweep.sh)")
     p.add_argument("--mode", default="parity", choices=["parity", "fast"],
                    help="fast = BZR_MODE_FAST Newton stage (contracted FMA, approximate div/sqrt; not bit-exact)")
     p.add_argument("--cpu-baseline", default="on", choices=["on", "off"])
@@ -338,8 +359,8 @@ def main():
 
     if launch.check_world(a.gpus) == "spawn":  # bare `bench.py --gpus N`: start the N rank processes here
         raise SystemExit(launch.spawn([sys.executable, str(Path(__file__).resolve())] + sys.argv[1:], a.gpus))
-    if a.inflight <= 0:  # the staged pipeline's small kernels contend beyond two frames
-        a.inflight = 3 if (a.accel == "bvh" and a.pipeline == "fused") else 2
+    if a.inflight <= 0:
+        a.inflight = default_inflight(a, int(os.environ.get("WORLD_SIZE", str(a.gpus))))
     hwq_source = set_hw_queues(a.inflight, int(os.environ.get("WORLD_SIZE", "1")))
     import torch
     import torch.distributed as dist

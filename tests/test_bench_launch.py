@@ -115,3 +115,26 @@ def test_parent_sigterm_stops_the_ranks(tmp_path):
     finally:
         if p.poll() is None:
             p.kill()
+
+
+def test_default_frames_in_flight_follow_the_rank_frame_size():
+    """--inflight 0: 6 slots for a rank frame of at most 4 M primaries, else 3 (fused) / 2 (staged)."""
+    sys.path.insert(0, str(REPO))
+    import bench
+
+    def slots(argv, world):
+        old = sys.argv
+        try:
+            sys.argv = ["bench.py"] + argv
+            return bench.default_inflight(bench.parse(), world)
+        finally:
+            sys.argv = old
+
+    assert slots(["--config", "cfg2"], 1) == 6
+    assert slots(["--config", "cfg3", "--pipeline", "staged"], 1) == 6
+    assert slots([], 1) == 3                                  # cfg4 4096², the N = 1 line
+    assert slots([], 2) == 3                                  # 8 M primaries per rank
+    assert slots([], 4) == 6 and slots([], 8) == 6            # strong-scaling shares
+    assert slots(["--scaling", "weak"], 8) == 3               # weak: every rank keeps 4096²
+    assert slots(["--config", "cfg5", "--pipeline", "staged"], 1) == 2
+    assert slots(["--config", "cfg4", "--side", "2048", "--pipeline", "staged"], 1) == 6
