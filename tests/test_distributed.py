@@ -146,15 +146,16 @@ def loop_worker(rank, world, port, width, height, patches, result_path, layout, 
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("layout", ["compact", "rays", "image"])
-def test_frame_loop_inflight_async_gather(bzr, orc, tmp_path, layout):
-    """frame.FrameLoop at world size 2 with 3 frames in flight and 5 frames: every frame lands on rank 0
-    once, under its own index, equal to a single-process trace of that frame; the compact layout delivers
-    every final ray in fewer bytes than the rays layout."""
+@pytest.mark.parametrize("layout,inflight,frames", [("compact", 3, 5), ("rays", 3, 5), ("image", 3, 5), ("image", 6, 8)])
+def test_frame_loop_inflight_async_gather(bzr, orc, tmp_path, layout, inflight, frames):
+    """frame.FrameLoop at world size 2 with 3 frames in flight and 5 frames (and, in the image layout, bench.py's
+    6 slots for small rank frames over 8 frames): every frame lands on rank 0 once, under its own index, equal to a
+    single-process trace of that frame; the compact layout delivers every final ray in fewer bytes than the rays
+    layout (DESIGN.md (e))."""
     cfg = CONFIGS["cfg2"]
     patches = bzr.TriMesh().make_ellipsoid(32, 16, (1, 4, 2)).translate((10, 0, 0)).standardize().bezier_patches()
     width = height = 128
-    world, inflight, frames = 2, 3, 5
+    world = 2
     out = tmp_path / "loop.npz"
     mp.start_processes(loop_worker, args=(world, free_port(), width, height, patches, str(out), layout, inflight, frames),
                        nprocs=world, join=True, start_method="spawn")
