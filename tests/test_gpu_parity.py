@@ -359,3 +359,24 @@ def test_culled_equals_bruteforce_cfg5_ill_conditioned(bzr, ctx, pipe):
     b = bzr.intersect(ctx, dm, rays, mode=bzr.ACCEL_NONE)
     assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
     assert (a.view(np.uint32)[11] == 4).mean() > 0.2
+
+
+@pytest.mark.slow
+def test_staged_ragged_chunks_equal_bruteforce(bzr, ctx, meshes):
+    """The staged pipeline over a batch of two chunks of unequal, non-wave-multiple length (2900^2 = 8 410 000 rays
+    against 8 M-ray chunks: the batch is split into 4 205 056 + 4 204 944 rays), intersect and the chain: every bit
+    equal to the brute-force scan, so no ray is lost or doubled at the chunk seam and each chunk starts from zeroed
+    counters and histogram."""
+    cfg = CONFIGS["cfg2"]
+    dm = bzr.DeviceMesh(ctx, meshes["cfg2"][0])
+    rays = grid_rays(cfg, side=2900)
+    assert rays.shape[1] == 8_410_000 > 1 << 23
+    a = bzr.intersect(ctx, dm, rays, mode=bzr.PIPELINE_STAGED)
+    b = bzr.intersect(ctx, dm, rays, mode=bzr.ACCEL_NONE)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    assert (a.view(np.uint32)[11] == 4).mean() > 0.2
+    del a, b
+    x = bzr.trace_chain(ctx, [dm], [1.3], rays, mode=bzr.PIPELINE_STAGED)
+    y = bzr.trace_chain(ctx, [dm], [1.3], rays, mode=bzr.ACCEL_NONE)
+    for p, q in zip(x, y):
+        assert np.array_equal(np.asarray(p).view(np.uint32), np.asarray(q).view(np.uint32))
