@@ -3404,6 +3404,26 @@ uint32_t hybrid_threshold() {
   return BZR_TRAV_HYBRID ? t : 0u;
 }
 
+// Grid of the persistent staged kernels (k_newton, k_resolve) in units of the device's resident capacity
+// (A/B knobs, environment BZR_NEWTON_GRIDX / BZR_RESOLVE_GRIDX, 1..64, read once per process; default 1).  A grid
+// of exactly the resident capacity holds every wave slot until the kernel ends, so another frame's kernels (frames
+// in flight, their own streams) cannot start beside it; k x capacity ends in k generations of blocks, between
+// which the dispatcher also takes the other streams' blocks.
+uint32_t env_scale(const char *name) {
+  const char *e = std::getenv(name);
+  if (!e || !*e) return 1u;
+  const long v = std::strtol(e, nullptr, 10);
+  return (uint32_t)(v < 1 ? 1 : v > 64 ? 64 : v);
+}
+uint32_t newton_gridx() {
+  static const uint32_t s = env_scale("BZR_NEWTON_GRIDX");
+  return s;
+}
+uint32_t resolve_gridx() {
+  static const uint32_t s = env_scale("BZR_RESOLVE_GRIDX");
+  return s;
+}
+
 // Workspace of the culled path for chunks of up to `chunk` rays over meshes of up to `nb` patches.
 using SplitIt = hipcub::TransformInputIterator<unsigned long long, BucketSplit, const uint32_t *>;
 bzr_status ensure_work(bzr_ctx *ctx, uint32_t chunk, uint32_t nb, Work &w) {
@@ -3514,14 +3534,14 @@ bzr_status run_culled(bzr_ctx *ctx, const MeshView &mv, const float *rays, uint3
   }
   // persistent grid: the resident capacity of the device, never more than the worst-case chunk count
   const uint32_t gn = std::min<uint32_t>(std::max<uint32_t>((kMaxCand * n + kBlock - 1) / kBlock, 1u),
-                                         resident_blocks(ctx, k_newton<kFast>));
+                                         resident_blocks(ctx, k_newton<kFast>) * newton_gridx());
   launch(ctx, BZR_KERNEL_NEWTON, k_newton<kFast>, dim3(gn), mv.full, w.offs + hn, w.pairs, rays, ld, off, n, w.slot, w.key,
          w.fol, w.ctr, (const float4 *)w.aos, w.ro);
   launch(ctx, BZR_KERNEL_NEWTON_LANE, k_newton_lane<kFast>, dim3(std::min<uint32_t>(std::max<uint32_t>(n / 1024u, 1u), 1024u)),
          mv.full, w.offs + hn, w.pairs, rays, ld, off, n, w.slot, w.key, w.fol, w.ctr, (const float4 *)w.aos, w.ro);
   {  // follow retries + overflow rays (whose keys the Newton stage left untouched: their lists are empty)
     const uint64_t items = (uint64_t)n * ((nb + kOvfSlice - 1) / kOvfSlice);
-    const uint32_t grid = std::max(std::min<uint32_t>(grid_for(n / 8 + 1), 1024u),
+    const uint32_t grid = std::max(std::min<uint32_t>(grid_for(n / 8 + 1), 1024u * resolve_gridx()),
                                    (uint32_t)std::min<uint64_t>(items, BZR_OVERFLOW_BLOCKS));
     launch(ctx, BZR_KERNEL_FOLLOW, k_resolve<kFast>, dim3(std::max<uint32_t>(grid, 1u)), mv, rays, ld, off, n, w);
   }
