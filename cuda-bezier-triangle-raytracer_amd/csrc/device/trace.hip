@@ -233,6 +233,12 @@ constexpr int kTravStack = BZR_TRAV_WIDE == 2 ? 4 * kStack : kStack;
 #ifndef BZR_OVERFLOW_BLOCKS
 #define BZR_OVERFLOW_BLOCKS 2048u
 #endif
+// BZR_NEWTON_QUEUE (A/B knob, default 0): k_newton's waves take their dense chunks from a work counter (w.ctr[5],
+// one atomic per chunk and wave) instead of the static stride q, q + W, ...: a wave that drew cheap chunks takes
+// more, so the kernel ends when the work does, not when its most loaded wave does.
+#ifndef BZR_NEWTON_QUEUE
+#define BZR_NEWTON_QUEUE 0
+#endif
 // BZR_NEWTON_GATED (default 1): k_newton skips the planar gate its pairs already passed in k_traverse.
 #ifndef BZR_NEWTON_GATED
 #define BZR_NEWTON_GATED 1
@@ -2014,7 +2020,11 @@ __global__ __launch_bounds__(kBlock) BZR_NEWTON_ATTR void k_newton(const float *
   uint2 pr2 = make_uint2(kNoPair, 0u);
   if (q + W < D) pr2 = pairs[(q + W) * 64u + lane];
 #endif
+#if BZR_NEWTON_QUEUE && !BZR_NEWTON_PREFETCH
+  for (uint32_t qnext = 0; q < D; q = qnext) {
+#else
   for (; q < D; q += W) {
+#endif
     const uint32_t p = q * 64u + lane;
     const bool todo = pr.x != kNoPair;
     const uint32_t ray = pr.x & kRayMask, j = pr.x >> 26;
@@ -2028,8 +2038,17 @@ __global__ __launch_bounds__(kBlock) BZR_NEWTON_ATTR void k_newton(const float *
 #else
     f3 s = mk(0.0f, 0.0f, 0.0f), d = s;
     if (todo) load_pair_ray(aos, rays, ld, off, ray, s, d);  // pairs of one patch: mostly neighbouring rays
-    const uint32_t qn = q + W;  // prefetch the next chunk's pair records
-    if (qn < D) pr = pairs[qn * 64u + lane];
+#if BZR_NEWTON_QUEUE
+    uint32_t qn = 0;  // the wave's next chunk: the W first chunks went to the waves by id, the rest from the counter
+    if (lane == 0u) qn = atomicAdd(nfol + 5, 1u);
+    qn = __builtin_amdgcn_readfirstlane(qn) + W;
+#else
+    const uint32_t qn = q + W;
+#endif
+    if (qn < D) pr = pairs[qn * 64u + lane];  // prefetch the next chunk's pair records
+#endif
+#if BZR_NEWTON_QUEUE && !BZR_NEWTON_PREFETCH
+    qnext = qn;
 #endif
     bool is_fol = false;
     const auto pa = uniform_patch(full, b);
@@ -2156,7 +2175,7 @@ template <int kMode, bool kFast>
 __global__ __launch_bounds__(kBlock) BZR_FINISH_ATTR void k_finish(MeshView m, const float *rays, uint32_t ld, uint32_t off, uint32_t n,
                                                    Work w, Out o) {
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  if (blockIdx.x == 0 && threadIdx.x < 5) w.ctr[threadIdx.x] = 0u;  // last reader of the counters this segment
+  if (blockIdx.x == 0 && threadIdx.x < 6) w.ctr[threadIdx.x] = 0u;  // last reader of the counters this segment
   if (i >= n) return;
   const uint32_t gi = off + i;
   if constexpr (kMode == kModeHits && BZR_FINISH_NORAY) {
@@ -3405,22 +3424,36 @@ uint32_t hybrid_threshold() {
 }
 
 // Grid of the persistent staged kernels (k_newton, k_resolve) in units of the device's resident capacity
-// (A/B knobs, environment BZR_NEWTON_GRIDX / BZR_RESOLVE_GRIDX, 1..64, read once per process; default 1).  A grid
+// (A/B knobs, environment BZR_NEWTON_GRIDX / BZR_RESOLVE_GRIDX, 1..64, read once per process).  A grid
 // of exactly the resident capacity holds every wave slot until the kernel ends, so another frame's kernels (frames
 // in flight, their own streams) cannot start beside it; k x capacity ends in k generations of blocks, between
 // which the dispatcher also takes the other streams' blocks.
-uint32_t env_scale(const char *name) {
+uint32_t env_scale(const char *name, uint32_t dflt = 1u) {
   const char *e = std::getenv(name);
-  if (!e || !*e) return 1u;
+  if (!e || !*e) return dflt;
   const long v = std::strtol(e, nullptr, 10);
   return (uint32_t)(v < 1 ? 1 : v > 64 ? 64 : v);
 }
-uint32_t newton_gridx() {
-  static const uint32_t s = env_scale("BZR_NEWTON_GRIDX");
-  return s;
+// k_newton: 2 x the resident capacity on meshes of at least 2^17 patches, else 1 x (BZR_NEWTON_GRIDX overrides).
+// Measured (profiles/r06_ab_gridx_cfg5.jsonl, same bits): cfg5 (301 056 patches, 8 M-ray chunks) k_newton 4.33 ->
+// 4.15 ms per lone frame and +0.8 to +1.5 % at bench level on three boxes, 4 x / 8 x / 16 x lose (every wave's
+// follow-list flush is an atomic on one counter); cfg3 (28 800 patches) k_newton 0.174 -> 0.205 ms lone, -1 to -2 %
+// at bench level.
+constexpr uint32_t kNewtonGrid2Patches = 1u << 17;
+uint32_t newton_gridx(uint32_t nb) {
+  static const uint32_t s = env_scale("BZR_NEWTON_GRIDX", 0u);
+  return s ? s : nb >= kNewtonGrid2Patches ? 2u : 1u;
 }
-uint32_t resolve_gridx() {
-  static const uint32_t s = env_scale("BZR_RESOLVE_GRIDX");
+// k_resolve's block cap: BZR_RESOLVE_BLOCKS (absolute, 64..65536) if set, else 1024 x BZR_RESOLVE_GRIDX
+uint32_t resolve_blocks() {
+  static const uint32_t s = [] {
+    const char *e = std::getenv("BZR_RESOLVE_BLOCKS");
+    if (e && *e) {
+      const long v = std::strtol(e, nullptr, 10);
+      return (uint32_t)(v < 64 ? 64 : v > 65536 ? 65536 : v);
+    }
+    return 1024u * env_scale("BZR_RESOLVE_GRIDX");
+  }();
   return s;
 }
 
@@ -3534,14 +3567,14 @@ bzr_status run_culled(bzr_ctx *ctx, const MeshView &mv, const float *rays, uint3
   }
   // persistent grid: the resident capacity of the device, never more than the worst-case chunk count
   const uint32_t gn = std::min<uint32_t>(std::max<uint32_t>((kMaxCand * n + kBlock - 1) / kBlock, 1u),
-                                         resident_blocks(ctx, k_newton<kFast>) * newton_gridx());
+                                         resident_blocks(ctx, k_newton<kFast>) * newton_gridx(nb));
   launch(ctx, BZR_KERNEL_NEWTON, k_newton<kFast>, dim3(gn), mv.full, w.offs + hn, w.pairs, rays, ld, off, n, w.slot, w.key,
          w.fol, w.ctr, (const float4 *)w.aos, w.ro);
   launch(ctx, BZR_KERNEL_NEWTON_LANE, k_newton_lane<kFast>, dim3(std::min<uint32_t>(std::max<uint32_t>(n / 1024u, 1u), 1024u)),
          mv.full, w.offs + hn, w.pairs, rays, ld, off, n, w.slot, w.key, w.fol, w.ctr, (const float4 *)w.aos, w.ro);
   {  // follow retries + overflow rays (whose keys the Newton stage left untouched: their lists are empty)
     const uint64_t items = (uint64_t)n * ((nb + kOvfSlice - 1) / kOvfSlice);
-    const uint32_t grid = std::max(std::min<uint32_t>(grid_for(n / 8 + 1), 1024u * resolve_gridx()),
+    const uint32_t grid = std::max(std::min<uint32_t>(grid_for(n / 8 + 1), resolve_blocks()),
                                    (uint32_t)std::min<uint64_t>(items, BZR_OVERFLOW_BLOCKS));
     launch(ctx, BZR_KERNEL_FOLLOW, k_resolve<kFast>, dim3(std::max<uint32_t>(grid, 1u)), mv, rays, ld, off, n, w);
   }
