@@ -1170,8 +1170,9 @@ __device__ __forceinline__ void rank_flush(RankPend &pr, const Work &w, uint32_t
 #ifndef BZR_TRAV_HYBRID
 #define BZR_TRAV_HYBRID 0
 #endif
-// BZR_TRAV_PRIO (A/B knob with BZR_TRAV_HYBRID, default 0): the walk at s_setprio(N), the in-wave passes at 0 (as
-// k_trace's BZR_TRACE_PRIO).
+// BZR_TRAV_PRIO (A/B knob, default 0): the walk at s_setprio(N) -- with BZR_TRAV_HYBRID the in-wave passes back at 0
+// (as k_trace's BZR_TRACE_PRIO); without it the whole k_traverse wave, ahead of the other frame's k_newton waves
+// that share its CUs when frames are in flight.
 #ifndef BZR_TRAV_PRIO
 #define BZR_TRAV_PRIO 0
 #endif
@@ -1258,7 +1259,7 @@ __device__ __forceinline__ void traverse_rays(const MeshView &m, const float *__
   uint32_t ph_cur = 0;
 #endif
   uint32_t c_nodes = 0, c_leaves = 0, c_gates = 0;  // work counters (with counters on; wave-uniform)
-#if BZR_TRAV_HYBRID && BZR_TRAV_PRIO
+#if BZR_TRAV_PRIO
   __builtin_amdgcn_s_setprio(BZR_TRAV_PRIO);  // the walk's chain of loads ahead of other waves' Newton passes
 #endif
   bool active = i < n && (alive == nullptr || alive[off + i] != BZR_RR_NONE);
