@@ -398,7 +398,11 @@ def main():
     upload_s = time.perf_counter() - t0
     # one stream per frame slot (--inflight); GPU_MAX_HW_QUEUES (top of this file) gives each its own
     # hardware queue, so the slots' frames overlap
-    streams = [torch.cuda.Stream(dev) for _ in range(max(1, a.inflight))]
+    # BZR_BENCH_SLOT_PRIO (A/B knob, default off): "lead" puts slot 0's stream at the device's highest stream
+    # priority, so the other slots' frames fill the tails of slot 0's kernels instead of contending with them
+    slot_prio = os.environ.get("BZR_BENCH_SLOT_PRIO", "")
+    top_prio = torch.cuda.Stream.priority_range()[1] if slot_prio == "lead" else 0
+    streams = [torch.cuda.Stream(dev, priority=top_prio if i == 0 else 0) for i in range(max(1, a.inflight))]
     hwq = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
     if hwq < len(streams) + (1 if world > 1 else 0) and rank == 0:
         print(f"bench.py: warning: GPU_MAX_HW_QUEUES={hwq} < {len(streams)} frame streams"
@@ -674,6 +678,7 @@ def main():
                 "frame_verified": verify["frame"],
                 "pipeline": a.pipeline,
                 "frames_in_flight": F,
+                **({"slot_priority": {"mode": slot_prio, "slot0": top_prio}} if slot_prio else {}),
                 "hw_queues": {"GPU_MAX_HW_QUEUES_requested": hwq, "source": hwq_source,
                               "streams": len(streams) + (1 if gather else 0),
                               "ok": hwq >= len(streams) + (1 if gather else 0)},
